@@ -1,0 +1,111 @@
+/*
+ * uno_kkt.h -- C ABI of the MI355X-native sparse symmetric-indefinite KKT backend.
+ *
+ * Drop-in boundary for Uno's linear-solver plugin surface (reference snapshot 2025-08-08):
+ *   uno/ingredients/subproblem_solvers/DirectSymmetricIndefiniteLinearSolver.hpp:11-25
+ *   uno/ingredients/subproblem_solvers/SymmetricIndefiniteLinearSolver.hpp:20-33
+ * The entry points below are exactly what the MUMPS adapter binds today
+ * (uno/ingredients/subproblem_solvers/MUMPS/MUMPSSolver.cpp); each one names the call it replaces.
+ * The C++ adapter that implements the Uno class on top of this ABI is in integration/ and
+ * INTEGRATION.md.  Plain pointers and sizes only; no torch or HIP types cross this boundary.
+ *
+ * Matrix contract: 0-based COO (row, col, value) triplets, either triangle, duplicates
+ * summed (MUMPS sym=2); the pattern is fixed between uno_kkt_analyze and every later factorization,
+ * only values change.  All arithmetic is IEEE binary64.
+ */
+#ifndef UNO_KKT_H
+#define UNO_KKT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* status codes */
+#define UNO_KKT_OK 0
+#define UNO_KKT_ERR_ARG (-1)      /* bad argument (size, index out of range, unknown option) */
+#define UNO_KKT_ERR_STATE (-2)    /* call out of order (factorize before analyze, ...) */
+#define UNO_KKT_ERR_HIP (-3)      /* HIP runtime error (message in uno_kkt_last_error) */
+#define UNO_KKT_ERR_PIVOT (-4)    /* a fully-summed column admits no pivot in its front */
+#define UNO_KKT_ERR_NOMEM (-5)    /* device allocation failed */
+#define UNO_KKT_ERR_NODEVICE (-6) /* no HIP device / extension not usable */
+
+typedef struct uno_kkt* uno_kkt_t;
+
+typedef struct {
+    int64_t n;              /* KKT dimension */
+    int64_t nnz;            /* COO entries (with duplicates) */
+    int64_t nnz_unique;     /* canonical lower-triangle entries */
+    int64_t nnz_L;          /* strictly-lower nonzeros of L as stored by the fronts (unpadded) */
+    int64_t n_fronts;       /* supernodes / frontal matrices */
+    int64_t n_levels;       /* assembly-tree levels (launch waves) */
+    int64_t max_front;      /* largest front order */
+    int64_t n_dense;        /* dense (arrow) nodes ordered last */
+    int64_t pivots_2x2;     /* last factorization */
+    int64_t pivots_null;    /* last factorization: null pivots (= zero eigenvalues) */
+    int64_t pivots_relaxed; /* last factorization: pivots accepted below the threshold u */
+    int64_t factorizations; /* counters since analysis */
+    int64_t solves;
+    double flops;           /* factorization flops (sum over fronts) */
+    double analysis_seconds;/* host wall time of the last uno_kkt_analyze */
+    double bytes_L;         /* 8 * stored factor entries (L + D) */
+    double bytes_cb;        /* 8 * contribution-block entries written per factorization */
+} uno_kkt_stats_t;
+
+/* Create a solver bound to HIP device `device_id`.  Replaces MUMPS JOB=-1 (MUMPSSolver.cpp:16-37). */
+int uno_kkt_create(uno_kkt_t* handle, int device_id);
+
+/* Release all host and device memory.  Replaces MUMPS JOB=-2 (MUMPSSolver.cpp:46-49). */
+void uno_kkt_destroy(uno_kkt_t handle);
+
+/* Options: "pivot_threshold" (u, default 0.01 = MUMPS CNTL(1) for sym=2),
+ * "null_tol_factor" (default 1e-5: thres = eps*1e-5*||A_pre||_inf, ICNTL(24)=1 with CNTL(3)=0),
+ * "scale_iters" (default 1, ICNTL(8)=8 restated), "leaf_size" (ND leaf, default 32),
+ * "max_block" (max supernode width, default 64), "timing" (1 = per-kernel HIP event timing). */
+int uno_kkt_set_option(uno_kkt_t handle, const char* name, double value);
+
+/* Symbolic analysis on a COO pattern (0-based, any triangle, duplicates allowed).  Host pointers.
+ * Replaces do_symbolic_analysis / JOB=1 (MUMPSSolver.cpp:72-83, save_sparsity_to_local_format :149-157). */
+int uno_kkt_analyze(uno_kkt_t handle, int64_t n, int64_t nnz, const int64_t* row, const int64_t* col);
+
+/* Numerical LDL^T factorization of the values in COO order (same order as the analysed pattern).
+ * values_on_device = 0: host pointer (copied H2D), 1: device pointer, and values == NULL reuses the
+ * device-resident values of the previous call (after uno_kkt_set_values / uno_kkt_fill_values).
+ * Replaces do_numerical_factorization / JOB=2 (MUMPSSolver.cpp:85-89). */
+int uno_kkt_factorize(uno_kkt_t handle, const double* values, int values_on_device);
+
+/* Device-side value edits between factorizations (the inertia-correction loop changes only the
+ * regularization diagonal: COOFormat::set_regularization, COOFormat.hpp:102-110). */
+int uno_kkt_set_values(uno_kkt_t handle, const int64_t* positions, const double* values, int64_t count);
+int uno_kkt_fill_values(uno_kkt_t handle, int64_t first_position, int64_t count, double value);
+
+/* Inertia of the last factorization.  Replaces get_inertia / INFOG(12) / INFOG(28)
+ * (MUMPSSolver.cpp:124-139).  Singular <=> zero > 0 (:141-143); rank = n - zero (:145-147). */
+int uno_kkt_inertia(uno_kkt_t handle, int64_t* positive, int64_t* negative, int64_t* zero);
+
+/* Solve K x = rhs with the last factorization (nrhs = 1).  on_device = 0: host pointers, 1: device
+ * pointers.  rhs and x may alias.  Replaces solve_indefinite_system / JOB=3 (MUMPSSolver.cpp:91-96). */
+int uno_kkt_solve(uno_kkt_t handle, const double* rhs, double* x, int on_device);
+
+/* Counters of the last analysis / factorization. */
+int uno_kkt_stats(uno_kkt_t handle, uno_kkt_stats_t* stats);
+
+/* Per-kernel-class device time accumulated while option "timing" is 1 (HIP events on the solver's
+ * stream).  names: comma-separated list written into `names` (size `cap`), ms/launches per class. */
+int uno_kkt_kernel_times(uno_kkt_t handle, char* names, int cap, double* ms, int64_t* launches, int max_classes);
+int uno_kkt_reset_kernel_times(uno_kkt_t handle);
+
+/* The hipStream_t the solver launches on (as void*), for callers that time or overlap work. */
+void* uno_kkt_stream(uno_kkt_t handle);
+
+/* Human-readable description of the last error on this handle ("" if none). */
+const char* uno_kkt_last_error(uno_kkt_t handle);
+
+/* Library version string. */
+const char* uno_kkt_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNO_KKT_H */

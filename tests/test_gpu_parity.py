@@ -1,0 +1,182 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the reference's known
+answers.  Integer results (inertia, singularity, rank) must match exactly; solutions are checked
+against the oracle and by residual, with tolerances stated in each test (north_star: primal/dual
+residuals within 1e-10 relative)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle_ffi import OracleKKT
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KATS = json.load(open(os.path.join(HERE, "golden", "kats.json")))
+RES_TOL = 1e-10  # relative residual ||Kx-b||_inf / (||K||_inf ||x||_inf + ||b||_inf)
+
+
+@pytest.fixture(scope="module")
+def uno_amd():
+    import uno_amd as ua
+    ua.load_library()
+    return ua
+
+
+def rel_residual(n, r, c, v, x, b):
+    from uno_amd import coo_symv
+    res = coo_symv(n, r, c, v, x) - b
+    absv = coo_symv(n, r, c, np.abs(v), np.ones(n))  # row sums of |K|
+    return np.abs(res).max() / (absv.max() * np.abs(x).max() + np.abs(b).max())
+
+
+def both(n, r, c, v, **opt):
+    from uno_amd import HipKKT
+    g = HipKKT(0, **opt)
+    g.analyze(n, r, c)
+    g.factorize(v)
+    o = OracleKKT()
+    o.analyze(n, r, c)
+    o.factorize(v)
+    return g, o
+
+
+def test_kat_5x5(uno_amd):
+    k = KATS["mumps_5x5"]
+    g, o = both(k["n"], k["rows"], k["cols"], k["vals"])
+    assert g.inertia() == tuple(k["inertia"]) == o.inertia()
+    np.testing.assert_allclose(g.solve(k["rhs"]), k["solution"], atol=k["solution_tol"], rtol=0)
+
+
+def test_kat_singular(uno_amd):
+    k = KATS["mumps_singular"]
+    g, o = both(k["n"], k["rows"], k["cols"], k["vals"])
+    assert g.inertia() == tuple(k["inertia"]) == o.inertia()
+    s = uno_amd.HipLDLSolver()
+    m = uno_amd.SparseSymmetricMatrix(k["n"], len(k["rows"]), 0)
+    for r, c, v in zip(k["rows"], k["cols"], k["vals"]):
+        m.insert(r, c, v)
+    s.initialize_memory(k["n"], 0, len(k["rows"]), 0)
+    s.do_symbolic_analysis(m)
+    s.do_numerical_factorization(m)
+    assert s.matrix_is_singular() and s.rank() == 2 and s.number_negative_eigenvalues() == 1
+
+
+@pytest.mark.parametrize("name", ["hs015_kkt0", "hs015_lsq"])
+def test_hs015_systems(uno_amd, name):
+    k = KATS[name]
+    g, o = both(k["n"], k["rows"], k["cols"], k["vals"])
+    assert g.inertia() == o.inertia()
+    b = np.arange(1.0, k["n"] + 1)
+    xg, xo = g.solve(b), o.solve(b)
+    np.testing.assert_allclose(xg, xo, rtol=1e-9, atol=1e-12)
+    assert rel_residual(k["n"], k["rows"], k["cols"], k["vals"], xg, b) < RES_TOL
+
+
+def test_hs015_inertia_correction_trace(uno_amd):
+    """PrimalDualRegularization loop (PrimalDualRegularization.hpp:133-219) driven by the GPU and by
+    the oracle must visit the same (delta_w, delta_c, inertia) sequence."""
+    from uno_amd import SparseSymmetricMatrix, HipLDLSolver, regularize_augmented_matrix
+    k = KATS["hs015_kkt0"]
+
+    class OracleSolver(HipLDLSolver):
+        def __init__(self):
+            self.kkt = None
+            self.o = OracleKKT()
+
+        def do_symbolic_analysis(self, m):
+            r, c, _ = m.arrays()
+            self.o.analyze(m.dimension(), r, c)
+
+        def do_numerical_factorization(self, m):
+            self.o.factorize(m.arrays()[2])
+
+        def get_inertia(self):
+            return self.o.inertia()
+
+        def number_zero_eigenvalues(self):
+            return self.o.inertia()[2]
+
+    traces = []
+    for solver in (HipLDLSolver(), OracleSolver()):
+        m = SparseSymmetricMatrix(k["n"], len(k["rows"]) - 6, 6)
+        for r, c, v in zip(k["rows"][6:], k["cols"][6:], k["vals"][6:]):
+            m.insert(r, c, v)
+        tr = []
+        regularize_augmented_matrix(m, range(4), range(2), 1e-2, (4, 2, 0), solver, {}, trace=tr)
+        traces.append(tr)
+    assert traces[0] == traces[1]
+    assert traces[0][-1][2] == (4, 2, 0)
+
+
+def random_sym(rng, n, dens, zero_diag_frac):
+    A = np.where(rng.random((n, n)) < dens, rng.standard_normal((n, n)), 0.0)
+    A = np.tril(A)
+    d = np.diag(A).copy()
+    d[rng.random(n) < zero_diag_frac] = 0.0
+    np.fill_diagonal(A, d)
+    r, c = np.nonzero(A)
+    rr = np.concatenate([r, np.arange(n)])
+    cc = np.concatenate([c, np.arange(n)])
+    vv = np.concatenate([A[r, c], np.zeros(n)])
+    return rr, cc, vv, A + A.T - np.diag(np.diag(A))
+
+
+@pytest.mark.parametrize("nmax,dens", [(40, 0.3), (150, 0.05), (300, 0.6)])
+def test_random_indefinite(uno_amd, nmax, dens):
+    """Random sparse/dense symmetric indefinite systems, including fronts beyond the LDS limit
+    (n up to 300 dense -> k_factor_global)."""
+    rng = np.random.default_rng(nmax)
+    done = 0
+    for trial in range(12):
+        n = int(rng.integers(max(2, nmax // 3), nmax + 1))
+        rr, cc, vv, S = random_sym(rng, n, dens, zero_diag_frac=0.5)
+        ev = np.linalg.eigvalsh(S)
+        if np.min(abs(ev)) < 1e-8 * max(1.0, abs(ev).max()):
+            continue
+        g, o = both(n, rr, cc, vv)
+        assert g.inertia() == o.inertia() == (int((ev > 0).sum()), int((ev < 0).sum()), 0)
+        b = rng.standard_normal(n)
+        xg = g.solve(b)
+        np.testing.assert_allclose(S @ xg, b, atol=1e-8 * np.linalg.cond(S) * np.abs(b).max())
+        done += 1
+    assert done >= 6
+
+
+def test_arrowband_c2(uno_amd):
+    """C2: arrowband KKT N=1e4; first factorization has wrong inertia (negative
+    curvature), so the values of one regularized retry are compared too."""
+    from uno_amd import arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(10000, SEEDS["C2"])
+    g, o = both(n, r, c, v)
+    assert g.inertia() == o.inertia()
+    xg = g.solve(b)
+    assert rel_residual(n, r, c, v, xg, b) < RES_TOL
+    np.testing.assert_allclose(xg, o.solve(b), rtol=1e-6, atol=1e-9 * np.abs(xg).max())
+    # device-side diagonal update (inertia correction): delta_w on the primal block, -delta_c dual
+    g.fill_values(0, nv, 1e-2)
+    g.fill_values(nv, m, -1e-9)
+    g.factorize()
+    v2 = v.copy()
+    v2[:nv] = 1e-2
+    v2[nv:n] = -1e-9
+    o.factorize(v2)
+    assert g.inertia() == o.inertia()
+    xg = g.solve(b)
+    assert rel_residual(n, r, c, v2, xg, b) < RES_TOL
+    st = g.stats()
+    assert st["n_dense"] == 6 and st["factorizations"] == 2
+
+
+def test_empty_and_tiny(uno_amd):
+    from uno_amd import HipKKT
+    g = HipKKT()
+    g.analyze(3, [], [])
+    g.factorize(np.zeros(0))
+    assert g.inertia() == (0, 0, 3)
+    np.testing.assert_array_equal(g.solve([1.0, 2.0, 3.0]), 0.0)
+    g.analyze(1, [0], [0])
+    g.factorize([-2.0])
+    assert g.inertia() == (0, 1, 0)
+    np.testing.assert_allclose(g.solve([4.0]), [-2.0])

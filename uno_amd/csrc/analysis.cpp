@@ -1,0 +1,419 @@
+// analysis.cpp -- host symbolic analysis: canonical pattern, nested dissection, supernodes,
+// assembly tree, device layout.  See analysis.hpp and DESIGN.md section 3.
+#include "analysis.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+
+namespace ukkt {
+namespace {
+
+struct Graph {
+    int32_t n = 0;
+    std::vector<int64_t> ap;
+    std::vector<int32_t> ai;
+};
+
+// Nested dissection by BFS level-set separators (George's automatic ND) on the non-dense subgraph.
+// Emits groups in postorder: [ND(A)] [ND(B)] [separator]; each group becomes >= 1 supernode.
+class Dissector {
+public:
+    Dissector(const Graph& g, const std::vector<char>& skip, int leaf)
+        : g_(g), skip_(skip), leaf_(leaf), mark_(g.n, -1), level_(g.n, 0), queue_(g.n) {}
+
+    void run(std::vector<int32_t>& order, std::vector<int32_t>& group_start) {
+        order_ = &order;
+        groups_ = &group_start;
+        std::vector<int32_t> all;
+        all.reserve(g_.n);
+        for (int32_t v = 0; v < g_.n; ++v)
+            if (!skip_[v]) all.push_back(v);
+        dissect(std::move(all));
+        flush_pending();
+    }
+
+private:
+    const Graph& g_;
+    const std::vector<char>& skip_;
+    int leaf_;
+    std::vector<int32_t> mark_, level_, queue_;
+    int32_t stamp_ = 0;
+    std::vector<int32_t>* order_ = nullptr;
+    std::vector<int32_t>* groups_ = nullptr;
+    std::vector<int32_t> pending_;  // small independent components merged into one leaf group
+
+    void emit(const std::vector<int32_t>& nodes) {
+        if (nodes.empty()) return;
+        groups_->push_back((int32_t)order_->size());
+        order_->insert(order_->end(), nodes.begin(), nodes.end());
+    }
+    void flush_pending() {
+        if (!pending_.empty()) { emit(pending_); pending_.clear(); }
+    }
+
+    // BFS inside the set marked `member`; returns number of visited nodes, fills queue_/level_
+    int32_t bfs(int32_t start, int32_t member, int32_t visit, int32_t& nlev) {
+        int32_t head = 0, tail = 0;
+        queue_[tail++] = start;
+        mark_[start] = visit;
+        level_[start] = 0;
+        nlev = 1;
+        while (head < tail) {
+            int32_t v = queue_[head++];
+            int32_t lv = level_[v] + 1;
+            for (int64_t p = g_.ap[v]; p < g_.ap[v + 1]; ++p) {
+                int32_t w = g_.ai[p];
+                if (mark_[w] != member) continue;  // not in set, or already visited this sweep
+                mark_[w] = visit;
+                level_[w] = lv;
+                if (lv + 1 > nlev) nlev = lv + 1;
+                queue_[tail++] = w;
+            }
+        }
+        return tail;
+    }
+
+    void dissect(std::vector<int32_t> S) {
+        const int32_t sz = (int32_t)S.size();
+        if (sz == 0) return;
+        if (sz <= leaf_) {
+            pending_.insert(pending_.end(), S.begin(), S.end());
+            if ((int)pending_.size() >= leaf_) flush_pending();
+            return;
+        }
+        // mark members, check connectivity
+        int32_t member = ++stamp_;
+        for (int32_t v : S) mark_[v] = member;
+        int32_t nlev = 0;
+        int32_t visit = ++stamp_;
+        int32_t reached = bfs(S[0], member, visit, nlev);
+        if (reached < sz) {
+            // split into connected components; each is dissected independently
+            std::vector<std::vector<int32_t>> comps;
+            comps.emplace_back(queue_.begin(), queue_.begin() + reached);
+            for (int32_t v : S) {
+                if (mark_[v] != member) continue;
+                int32_t vis = ++stamp_;
+                int32_t cnt = bfs(v, member, vis, nlev);
+                comps.emplace_back(queue_.begin(), queue_.begin() + cnt);
+            }
+            S.clear();
+            S.shrink_to_fit();
+            for (auto& c : comps) dissect(std::move(c));
+            return;
+        }
+        flush_pending();
+        // pseudo-peripheral node: farthest node of a sweep, lowest degree in the last level
+        int32_t start = S[0];
+        for (int it = 0; it < 2; ++it) {
+            int32_t best = -1;
+            for (int32_t q = 0; q < reached; ++q) {
+                int32_t v = queue_[q];
+                if (level_[v] != nlev - 1) continue;
+                if (best < 0 || g_.ap[v + 1] - g_.ap[v] < g_.ap[best + 1] - g_.ap[best]) best = v;
+            }
+            for (int32_t v : S) mark_[v] = member;
+            visit = ++stamp_;
+            int32_t nl2 = 0;
+            bfs(best, member, visit, nl2);
+            bool improved = nl2 > nlev;
+            start = best;
+            nlev = nl2;
+            if (!improved) break;
+        }
+        (void)start;
+        if (nlev < 3) {  // no separating level: one (possibly wide) group
+            emit(S);
+            return;
+        }
+        std::vector<int32_t> cnt(nlev + 1, 0);
+        for (int32_t v : S) cnt[level_[v]]++;
+        int32_t acc = 0, lmed = 1;
+        for (int32_t l = 0; l < nlev; ++l) {
+            acc += cnt[l];
+            if (2 * acc >= sz) { lmed = l; break; }
+        }
+        lmed = std::min(std::max(lmed, 1), nlev - 2);
+        int32_t best = lmed;
+        for (int32_t l = std::max(1, lmed - 3); l <= std::min(nlev - 2, lmed + 3); ++l)
+            if (cnt[l] < cnt[best] || (cnt[l] == cnt[best] && std::abs(l - lmed) < std::abs(best - lmed)))
+                best = l;
+        const int32_t L = best;
+        std::vector<int32_t> A, B, sep;
+        A.reserve(sz / 2 + 1);
+        B.reserve(sz / 2 + 1);
+        for (int32_t v : S) {
+            int32_t lv = level_[v];
+            if (lv < L) A.push_back(v);
+            else if (lv > L) B.push_back(v);
+            else {
+                // keep only separator nodes that touch the far side
+                bool touches = false;
+                for (int64_t p = g_.ap[v]; p < g_.ap[v + 1] && !touches; ++p) {
+                    int32_t w = g_.ai[p];
+                    touches = mark_[w] == visit && level_[w] == L + 1;
+                }
+                (touches ? sep : A).push_back(v);
+            }
+        }
+        S.clear();
+        S.shrink_to_fit();
+        dissect(std::move(A));
+        flush_pending();
+        dissect(std::move(B));
+        flush_pending();
+        emit(sep);
+    }
+};
+
+}  // namespace
+
+std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
+                    const AnalysisOptions& opt, Symbolic& S) {
+    S = Symbolic();
+    if (n < 0 || nnz < 0) return "negative size";
+    if (n >= (int64_t(1) << 31) - 1 || nnz >= (int64_t(1) << 31) - 1) return "n or nnz exceeds int32 range";
+    for (int64_t k = 0; k < nnz; ++k)
+        if (row[k] < 0 || row[k] >= n || col[k] < 0 || col[k] >= n)
+            return "COO entry " + std::to_string(k) + " out of range";
+    S.n = n;
+    S.nnz = nnz;
+    const int32_t N = (int32_t)n;
+
+    // ---- canonical lower pattern: bucket by min index, sort by (max index, position) ----
+    std::vector<int64_t> bstart(n + 1, 0);
+    for (int64_t k = 0; k < nnz; ++k) bstart[std::min(row[k], col[k]) + 1]++;
+    for (int64_t i = 0; i < n; ++i) bstart[i + 1] += bstart[i];
+    std::vector<std::pair<int32_t, int32_t>> pr(nnz);
+    {
+        std::vector<int64_t> fill(bstart.begin(), bstart.end() - 1);
+        for (int64_t k = 0; k < nnz; ++k) {
+            int64_t b = std::min(row[k], col[k]), a = std::max(row[k], col[k]);
+            pr[fill[b]++] = {(int32_t)a, (int32_t)k};
+        }
+    }
+    std::vector<int32_t> ur, uc, udp;  // unique rows/cols, first position in pr
+    ur.reserve(nnz);
+    uc.reserve(nnz);
+    udp.reserve(nnz + 1);
+    for (int64_t b = 0; b < n; ++b) {
+        auto first = pr.begin() + bstart[b], last = pr.begin() + bstart[b + 1];
+        if (last - first > 1) std::sort(first, last);
+        for (auto it = first; it != last; ++it) {
+            if (it == first || it->first != (it - 1)->first) {
+                ur.push_back(it->first);
+                uc.push_back((int32_t)b);
+                udp.push_back((int32_t)(it - pr.begin()));
+            }
+        }
+    }
+    const int64_t nu = (int64_t)ur.size();
+    udp.push_back((int32_t)nnz);
+    S.nu = nu;
+
+    // ---- adjacency (no diagonal) ----
+    Graph g;
+    g.n = N;
+    g.ap.assign(n + 1, 0);
+    for (int64_t u = 0; u < nu; ++u)
+        if (ur[u] != uc[u]) { g.ap[ur[u] + 1]++; g.ap[uc[u] + 1]++; }
+    for (int64_t i = 0; i < n; ++i) g.ap[i + 1] += g.ap[i];
+    g.ai.resize(g.ap[n]);
+    {
+        std::vector<int64_t> pos(g.ap.begin(), g.ap.end() - 1);
+        for (int64_t u = 0; u < nu; ++u)
+            if (ur[u] != uc[u]) { g.ai[pos[ur[u]]++] = uc[u]; g.ai[pos[uc[u]]++] = ur[u]; }
+    }
+
+    // ---- ordering: dense nodes last, nested dissection on the rest ----
+    std::vector<char> dense(n, 0);
+    const double dthr = std::max(16.0, opt.dense_factor * std::sqrt((double)n));
+    for (int32_t v = 0; v < N; ++v)
+        if ((double)(g.ap[v + 1] - g.ap[v]) > dthr) { dense[v] = 1; S.n_dense++; }
+    std::vector<int32_t> order;
+    order.reserve(n);
+    std::vector<int32_t> group_start;
+    Dissector(g, dense, std::max(1, opt.leaf_size)).run(order, group_start);
+    if (S.n_dense) {
+        group_start.push_back((int32_t)order.size());
+        for (int32_t v = 0; v < N; ++v) if (dense[v]) order.push_back(v);
+    }
+    if ((int64_t)order.size() != n) return "internal: ordering is not a permutation";
+    group_start.push_back(N);
+    S.perm = order;
+    S.iperm.assign(n, -1);
+    for (int32_t q = 0; q < N; ++q) S.iperm[S.perm[q]] = q;
+
+    // ---- supernodes: each group cut into blocks of at most max_block columns ----
+    std::vector<int32_t> bfirst;
+    for (size_t gi = 0; gi + 1 < group_start.size(); ++gi) {
+        int32_t s = group_start[gi], e = group_start[gi + 1];
+        int32_t len = e - s;
+        if (len <= 0) continue;
+        int32_t nb = (len + opt.max_block - 1) / opt.max_block;
+        for (int32_t b = 0; b < nb; ++b) bfirst.push_back(s + (int32_t)((int64_t)len * b / nb));
+    }
+    bfirst.push_back(N);
+    const int32_t nf = (int32_t)bfirst.size() - 1;
+    S.nf = nf;
+    std::vector<int32_t> blk(n);
+    for (int32_t b = 0; b < nf; ++b)
+        for (int32_t j = bfirst[b]; j < bfirst[b + 1]; ++j) blk[j] = b;
+
+    // ---- block symbolic factorization (struct = rows beyond the block, new numbering) ----
+    std::vector<int64_t> soff(nf + 1, 0);
+    std::vector<int32_t> sidx;
+    S.f_parent.assign(nf, -1);
+    std::vector<std::vector<int32_t>> children(nf);
+    {
+        std::vector<int32_t> mark(n, -1), buf;
+        buf.reserve(1024);
+        for (int32_t b = 0; b < nf; ++b) {
+            const int32_t first = bfirst[b], last = bfirst[b + 1] - 1;
+            buf.clear();
+            for (int32_t j = first; j <= last; ++j) {
+                int32_t v = S.perm[j];
+                for (int64_t p = g.ap[v]; p < g.ap[v + 1]; ++p) {
+                    int32_t i = S.iperm[g.ai[p]];
+                    if (i > last && mark[i] != b) { mark[i] = b; buf.push_back(i); }
+                }
+            }
+            for (int32_t c : children[b])
+                for (int64_t q = soff[c]; q < soff[c + 1]; ++q) {
+                    int32_t i = sidx[q];
+                    if (i > last && mark[i] != b) { mark[i] = b; buf.push_back(i); }
+                }
+            std::sort(buf.begin(), buf.end());
+            sidx.insert(sidx.end(), buf.begin(), buf.end());
+            soff[b + 1] = (int64_t)sidx.size();
+            if (!buf.empty()) {
+                int32_t par = blk[buf[0]];
+                S.f_parent[b] = par;
+                children[par].push_back(b);
+            }
+        }
+    }
+
+    // ---- front descriptors ----
+    S.f_m.resize(nf);
+    S.f_p.resize(nf);
+    S.f_level.assign(nf, 0);
+    S.f_rows_off.assign(nf + 1, 0);
+    S.f_L_off.assign(nf + 1, 0);
+    S.f_cb_off.assign(nf + 1, 0);
+    S.f_child_off.assign(nf + 1, 0);
+    for (int32_t b = 0; b < nf; ++b) {
+        int64_t p = bfirst[b + 1] - bfirst[b];
+        int64_t m = p + (soff[b + 1] - soff[b]);
+        if (m > 65535) return "front order exceeds 65535";
+        S.f_m[b] = (int32_t)m;
+        S.f_p[b] = (int32_t)p;
+        S.max_m = std::max<int64_t>(S.max_m, m);
+        S.f_rows_off[b + 1] = S.f_rows_off[b] + m;
+        S.f_L_off[b + 1] = S.f_L_off[b] + p * m - p * (p - 1) / 2;
+        int64_t cm = m - p;
+        S.f_cb_off[b + 1] = S.f_cb_off[b] + cm * (cm + 1) / 2;
+        S.nnz_L += p * (m - p) + p * (p - 1) / 2;
+        for (int64_t k = 0; k < p; ++k) {
+            double r = (double)(m - k - 1);
+            S.flops += r + r * (r + 1.0);
+        }
+        for (int32_t c : children[b]) S.f_level[b] = std::max(S.f_level[b], S.f_level[c] + 1);
+        S.f_child_off[b + 1] = S.f_child_off[b] + (int32_t)children[b].size();
+    }
+    S.L_size = S.f_L_off[nf];
+    S.cb_size = S.f_cb_off[nf];
+    S.rows.resize(S.f_rows_off[nf]);
+    for (int32_t b = 0; b < nf; ++b) {
+        int64_t o = S.f_rows_off[b];
+        for (int32_t j = bfirst[b]; j < bfirst[b + 1]; ++j) S.rows[o++] = S.perm[j];
+        for (int64_t q = soff[b]; q < soff[b + 1]; ++q) S.rows[o++] = S.perm[sidx[q]];
+    }
+    S.child.reserve(S.f_child_off[nf]);
+    for (int32_t b = 0; b < nf; ++b) S.child.insert(S.child.end(), children[b].begin(), children[b].end());
+
+    // local row of new index i inside front b
+    auto local_row = [&](int32_t b, int32_t i) -> int32_t {
+        if (i >= bfirst[b] && i < bfirst[b + 1]) return i - bfirst[b];
+        auto first = sidx.begin() + soff[b], last = sidx.begin() + soff[b + 1];
+        auto it = std::lower_bound(first, last, i);
+        if (it == last || *it != i) return -1;
+        return (int32_t)(S.f_p[b] + (it - first));
+    };
+
+    // ---- extend-add maps: contribution-block row of child -> parent local row ----
+    S.f_relmap_off.assign(nf + 1, 0);
+    for (int32_t b = 0; b < nf; ++b) S.f_relmap_off[b + 1] = S.f_relmap_off[b] + (soff[b + 1] - soff[b]);
+    S.relmap.resize(S.f_relmap_off[nf]);
+    for (int32_t b = 0; b < nf; ++b) {
+        int32_t par = S.f_parent[b];
+        for (int64_t q = soff[b]; q < soff[b + 1]; ++q) {
+            int32_t lr = par >= 0 ? local_row(par, sidx[q]) : -1;
+            if (lr < 0) return "internal: contribution row missing from parent front";
+            S.relmap[S.f_relmap_off[b] + (q - soff[b])] = lr;
+        }
+    }
+
+    // ---- packed value slots, front-major ----
+    S.f_ent_off.assign(nf + 1, 0);
+    std::vector<int32_t> ublk(nu);
+    for (int64_t u = 0; u < nu; ++u) {
+        int32_t a = S.iperm[ur[u]], c = S.iperm[uc[u]];
+        ublk[u] = blk[std::min(a, c)];
+        S.f_ent_off[ublk[u] + 1]++;
+    }
+    for (int32_t b = 0; b < nf; ++b) S.f_ent_off[b + 1] += S.f_ent_off[b];
+    S.ent_r.resize(nu);
+    S.ent_c.resize(nu);
+    S.ent_lpos.resize(nu);
+    S.identity_dups = (nu == nnz);
+    S.dup_ptr.assign(S.identity_dups ? 0 : nu + 1, 0);
+    S.dup_pos.resize(nnz);
+    {
+        std::vector<int64_t> fill(S.f_ent_off.begin(), S.f_ent_off.end() - 1);
+        std::vector<int32_t> slot_of(nu);
+        for (int64_t u = 0; u < nu; ++u) slot_of[u] = (int32_t)fill[ublk[u]]++;
+        for (int64_t u = 0; u < nu; ++u) {
+            int32_t s = slot_of[u], b = ublk[u];
+            int32_t a = S.iperm[ur[u]], c = S.iperm[uc[u]];
+            int32_t hi = std::max(a, c), lo = std::min(a, c);
+            int32_t lc = lo - bfirst[b];
+            int32_t lr = local_row(b, hi);
+            if (lr < 0) return "internal: entry row missing from its front";
+            S.ent_r[s] = S.perm[hi];
+            S.ent_c[s] = S.perm[lo];
+            S.ent_lpos[s] = ((uint32_t)lr << 16) | (uint32_t)lc;
+            if (!S.identity_dups) S.dup_ptr[s + 1] = udp[u + 1] - udp[u];
+        }
+        if (S.identity_dups) {
+            for (int64_t u = 0; u < nu; ++u) S.dup_pos[slot_of[u]] = pr[udp[u]].second;
+        } else {
+            for (int64_t s = 0; s < nu; ++s) S.dup_ptr[s + 1] += S.dup_ptr[s];
+            for (int64_t u = 0; u < nu; ++u) {
+                int64_t o = S.dup_ptr[slot_of[u]];
+                for (int32_t q = udp[u]; q < udp[u + 1]; ++q) S.dup_pos[o++] = pr[q].second;  // ascending COO position
+            }
+        }
+    }
+
+    // ---- level schedule ----
+    int32_t maxlev = 0;
+    for (int32_t b = 0; b < nf; ++b) maxlev = std::max(maxlev, S.f_level[b]);
+    S.nlevels = nf ? maxlev + 1 : 0;
+    S.level_off.assign(S.nlevels + 1, 0);
+    for (int32_t b = 0; b < nf; ++b) S.level_off[S.f_level[b] + 1]++;
+    for (int l = 0; l < S.nlevels; ++l) S.level_off[l + 1] += S.level_off[l];
+    S.level_fronts.resize(nf);
+    {
+        std::vector<int32_t> fill(S.level_off.begin(), S.level_off.end() - 1);
+        for (int32_t b = 0; b < nf; ++b) S.level_fronts[fill[S.f_level[b]]++] = b;
+        for (int l = 0; l < S.nlevels; ++l)
+            std::stable_sort(S.level_fronts.begin() + S.level_off[l], S.level_fronts.begin() + S.level_off[l + 1],
+                             [&](int32_t a, int32_t b) { return S.f_m[a] > S.f_m[b]; });
+    }
+    return "";
+}
+
+}  // namespace ukkt

@@ -1,0 +1,59 @@
+// analysis.hpp -- host-side symbolic analysis for the MI355X KKT backend.
+//
+// Replaces the symbolic phase Uno delegates to MUMPS JOB=1
+// (uno/ingredients/subproblem_solvers/MUMPS/MUMPSSolver.cpp:72-83): canonicalises the COO pattern
+// that uno/linear_algebra/COOFormat.hpp produces (duplicates, either triangle), orders it with
+// nested dissection (dense "arrow" rows last), groups columns into supernodes, and lays out every
+// device array the numerical phase reads: packed value slots per front, front row lists, extend-add
+// maps, factor / contribution-block arenas and the level schedule.  Runs once per pattern
+// (contract invariant 1 of SURVEY.md 8(b)).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace ukkt {
+
+struct AnalysisOptions {
+    int leaf_size = 32;   // nested-dissection leaf (nodes)
+    int max_block = 64;   // widest supernode (fully-summed columns per front)
+    double dense_factor = 10.0;  // dense node: degree > max(16, dense_factor * sqrt(n))
+};
+
+struct Symbolic {
+    int64_t n = 0, nnz = 0, nu = 0;
+    // packed value slots: slot s holds unique entry (ent_r[s], ent_c[s]) in original numbering,
+    // its value is the sum of COO positions dup_pos[dup_ptr[s] .. dup_ptr[s+1])
+    bool identity_dups = false;        // every unique entry has exactly one COO position
+    std::vector<int32_t> dup_ptr, dup_pos;
+    std::vector<int32_t> ent_r, ent_c; // original ids, ent_r is the later-eliminated one
+    std::vector<uint32_t> ent_lpos;    // (local row << 16) | local col inside the owning front
+    // ordering (new index -> original index and inverse)
+    std::vector<int32_t> perm, iperm;
+    int64_t n_dense = 0;
+    // fronts (supernodes), children have smaller ids than parents
+    int64_t nf = 0;
+    std::vector<int32_t> f_m, f_p, f_parent, f_level;
+    std::vector<int64_t> f_rows_off;   // nf+1, into rows
+    std::vector<int32_t> rows;         // original ids: fully-summed columns then struct rows
+    std::vector<int64_t> f_ent_off;    // nf+1, packed slot ranges
+    std::vector<int32_t> f_child_off;  // nf+1, into child
+    std::vector<int32_t> child;
+    std::vector<int64_t> f_relmap_off; // per front (as a child): cb_m entries into relmap
+    std::vector<int32_t> relmap;       // contribution-block row -> parent local row
+    std::vector<int64_t> f_L_off;      // packed lower trapezoid, m x p, column-major
+    std::vector<int64_t> f_cb_off;     // packed lower triangle, (m-p) x (m-p), column-major
+    int64_t L_size = 0, cb_size = 0, nnz_L = 0;
+    double flops = 0.0;
+    int64_t max_m = 0;
+    int nlevels = 0;
+    std::vector<int32_t> level_off;    // nlevels+1
+    std::vector<int32_t> level_fronts; // fronts by level, each level sorted by m descending
+};
+
+// Returns "" on success, an error message otherwise.
+std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
+                    const AnalysisOptions& opt, Symbolic& out);
+
+}  // namespace ukkt

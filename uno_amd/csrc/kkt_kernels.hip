@@ -1,0 +1,630 @@
+// kkt_kernels.hip -- hand-written CDNA4 (gfx950) kernels of the sparse KKT LDL^T backend.
+//
+// Numerical phase that Uno delegates to MUMPS JOB=2 / JOB=3
+// (uno/ingredients/subproblem_solvers/MUMPS/MUMPSSolver.cpp:85-96):
+//   k_pack          COO values -> packed per-front slots (duplicates summed, MUMPS sym=2), row maxima
+//   k_scale*        symmetric infinity-norm equilibration (ICNTL(8)=8 restated), ||A_pre||_inf
+//   k_factor_lds<MR> one workgroup per front: assemble + extend-add + threshold 1x1/2x2 LDL^T in LDS
+//   k_factor_global  same algorithm for fronts too large for LDS (front lives in HBM scratch)
+//   k_solve_fwd / k_solve_bwd  level-scheduled multifrontal triangular solves (nrhs = 1)
+// Every front is processed by one 256-thread workgroup (4 waves of 64); pivot search runs in wave 0
+// with butterfly shuffles, the rank-1/rank-2 Schur updates are spread over a 16x16 thread grid.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "kkt_kernels.hpp"
+
+namespace ukkt {
+
+constexpr int kThreads = 256;
+
+enum : int8_t { PIV_NULL = 0, PIV_1X1 = 1, PIV_2X2_A = 2, PIV_2X2_B = 3, PIV_STUCK = 4 };
+
+__device__ __forceinline__ double as_double(unsigned long long b) { return __longlong_as_double((long long)b); }
+__device__ __forceinline__ unsigned long long as_bits(double d) { return (unsigned long long)__double_as_longlong(d); }
+
+// ------------------------------------------------------------------------------------------------
+// pack + scaling
+// ------------------------------------------------------------------------------------------------
+
+__global__ void k_pack(const double* __restrict__ values, const int32_t* __restrict__ dup_ptr,
+                       const int32_t* __restrict__ dup_pos, const int32_t* __restrict__ ent_r,
+                       const int32_t* __restrict__ ent_c, int64_t nu, double* __restrict__ uval,
+                       unsigned long long* __restrict__ rmax) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
+        double v;
+        if (dup_ptr == nullptr) {
+            v = values[dup_pos[s]];
+        } else {
+            v = 0.0;
+            for (int32_t q = dup_ptr[s]; q < dup_ptr[s + 1]; ++q) v += values[dup_pos[q]];
+        }
+        uval[s] = v;
+        if (rmax) {
+            unsigned long long b = as_bits(fabs(v));
+            atomicMax(rmax + ent_r[s], b);
+            atomicMax(rmax + ent_c[s], b);
+        }
+    }
+}
+
+// rmax of the currently scaled matrix (sweeps 2.. of the equilibration)
+__global__ void k_rowmax_scaled(const double* __restrict__ uval, const int32_t* __restrict__ ent_r,
+                                const int32_t* __restrict__ ent_c, const double* __restrict__ scale, int64_t nu,
+                                unsigned long long* __restrict__ rmax) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
+        int32_t r = ent_r[s], c = ent_c[s];
+        unsigned long long b = as_bits(fabs(scale[r] * uval[s] * scale[c]));
+        atomicMax(rmax + r, b);
+        atomicMax(rmax + c, b);
+    }
+}
+
+__global__ void k_scale_update(const unsigned long long* __restrict__ rmax, double* __restrict__ scale, int64_t n,
+                               int first) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double r = as_double(rmax[i]);
+        double s = first ? 1.0 : scale[i];
+        if (r > 0.0) s = s / sqrt(r);
+        scale[i] = s;
+    }
+}
+
+__global__ void k_rowsum(const double* __restrict__ uval, const int32_t* __restrict__ ent_r,
+                         const int32_t* __restrict__ ent_c, const double* __restrict__ scale, int64_t nu,
+                         double* __restrict__ rowsum) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
+        int32_t r = ent_r[s], c = ent_c[s];
+        double w = fabs(scale[r] * uval[s] * scale[c]);
+        atomicAdd(rowsum + r, w);
+        if (r != c) atomicAdd(rowsum + c, w);
+    }
+}
+
+__global__ void k_normmax(const double* __restrict__ rowsum, int64_t n, unsigned long long* __restrict__ anorm) {
+    __shared__ double red[kThreads / 64];
+    double mx = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        mx = fmax(mx, rowsum[i]);
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kThreads / 64; ++w) mx = fmax(mx, red[w]);
+        atomicMax(anorm, as_bits(mx));
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
+// dense front factorization
+// ------------------------------------------------------------------------------------------------
+
+struct PivotDecision {
+    int kind;  // PIV_*
+    int c, r;  // candidate, 2x2 partner
+    int relaxed;
+};
+
+// |A(i,c)| with lower-triangle storage
+__device__ __forceinline__ double absA(const double* F, int ld, int i, int c) {
+    return fabs(i >= c ? F[i * ld + c] : F[c * ld + i]);
+}
+
+// Threshold pivot search (MUMPS/Duff-Reid rule, u then relaxed); run by one full wave, result in
+// every lane.  Mirrors test_pivot() of oracle/kkt_oracle.c; with no delayed pivots the threshold is
+// relaxed instead of delaying.
+__device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int p, double u, double thres) {
+    const int lane = threadIdx.x & 63;
+    PivotDecision d{PIV_STUCK, k, -1, 0};
+    for (int ul = 0; ul < 6; ++ul) {
+        // relaxation ladder u, u/10, u/100, 1e-6, 1e-10, 0 (no array: avoids scratch)
+        const double uu = ul == 0 ? u : ul == 1 ? u * 0.1 : ul == 2 ? u * 0.01 : ul == 3 ? 1e-6 : ul == 4 ? 1e-10 : 0.0;
+        for (int c = k; c < p; ++c) {
+            double g = 0.0, rv = 0.0;
+            int ri = 0x7fffffff;
+            for (int i = k + lane; i < m; i += 64) {
+                if (i == c) continue;
+                double v = absA(F, ld, i, c);
+                g = fmax(g, v);
+                if (i < p && v > rv) { rv = v; ri = i; }
+            }
+            for (int off = 32; off > 0; off >>= 1) {
+                g = fmax(g, __shfl_xor(g, off));
+                double orv = __shfl_xor(rv, off);
+                int ori = __shfl_xor(ri, off);
+                if (orv > rv || (orv == rv && ori < ri)) { rv = orv; ri = ori; }
+            }
+            const double acc = fabs(F[c * ld + c]);
+            if (fmax(acc, g) <= thres) { d.kind = PIV_NULL; d.c = c; d.relaxed = ul > 0; return d; }
+            if (acc != 0.0 && acc >= uu * g) { d.kind = PIV_1X1; d.c = c; d.relaxed = ul > 0; return d; }
+            if (rv > 0.0 && ri < p) {
+                const int r = ri;
+                double gc = 0.0, gr = 0.0;
+                for (int i = k + lane; i < m; i += 64) {
+                    if (i == c || i == r) continue;
+                    gc = fmax(gc, absA(F, ld, i, c));
+                    gr = fmax(gr, absA(F, ld, i, r));
+                }
+                for (int off = 32; off > 0; off >>= 1) {
+                    gc = fmax(gc, __shfl_xor(gc, off));
+                    gr = fmax(gr, __shfl_xor(gr, off));
+                }
+                const double a = F[c * ld + c];
+                const double b = r > c ? F[r * ld + c] : F[c * ld + r];
+                const double e = F[r * ld + r];
+                const double det = a * e - b * b;
+                if (det != 0.0) {
+                    const double lim = uu > 0.0 ? fabs(det) / uu : INFINITY;
+                    if (fabs(e) * gc + fabs(b) * gr <= lim && fabs(b) * gc + fabs(a) * gr <= lim) {
+                        d.kind = PIV_2X2_A; d.c = c; d.r = r; d.relaxed = ul > 0;
+                        return d;
+                    }
+                }
+            }
+        }
+    }
+    return d;
+}
+
+// symmetric interchange of positions a < b (lower-triangle storage), all threads
+__device__ void sym_swap(double* F, int ld, int m, int a, int b, int32_t* lrow) {
+    for (int t = threadIdx.x; t < m; t += blockDim.x) {
+        if (t < a) {
+            double x = F[a * ld + t]; F[a * ld + t] = F[b * ld + t]; F[b * ld + t] = x;
+        } else if (t == a) {
+            double x = F[a * ld + a]; F[a * ld + a] = F[b * ld + b]; F[b * ld + b] = x;
+            int32_t y = lrow[a]; lrow[a] = lrow[b]; lrow[b] = y;
+        } else if (t < b) {
+            double x = F[t * ld + a]; F[t * ld + a] = F[b * ld + t]; F[b * ld + t] = x;
+        } else if (t > b) {
+            double x = F[t * ld + a]; F[t * ld + a] = F[t * ld + b]; F[t * ld + b] = x;
+        }
+    }
+}
+
+// Schur update of the trailing lower triangle after a 1x1 (TWO=false) or 2x2 pivot at k.
+// LDS variant: 16x16 thread grid, MR rows/cols per thread kept in registers.
+template <int MR, bool TWO>
+__device__ __forceinline__ void schur_update_tile(double* F, int ld, int m, int k, double d0, double d1, double d2) {
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    const int r0 = k + (TWO ? 2 : 1);
+    double ci0[MR], ci1[MR], lj0[MR], lj1[MR];
+#pragma unroll
+    for (int a = 0; a < MR; ++a) {
+        int i = r0 + ty + 16 * a;
+        int j = r0 + tx + 16 * a;
+        ci0[a] = i < m ? F[i * ld + k] : 0.0;
+        ci1[a] = (TWO && i < m) ? F[i * ld + k + 1] : 0.0;
+        double x0 = j < m ? F[j * ld + k] : 0.0;
+        double x1 = (TWO && j < m) ? F[j * ld + k + 1] : 0.0;
+        if (TWO) {  // [l0 l1] = [x0 x1] * inv([[d0 d1][d1 d2]])
+            lj0[a] = d2 * x0 - d1 * x1;  // scaled by 1/det below (d-values pre-divided by det)
+            lj1[a] = d0 * x1 - d1 * x0;
+        } else {
+            lj0[a] = x0 * d0;  // d0 = 1/pivot
+            lj1[a] = 0.0;
+        }
+    }
+#pragma unroll
+    for (int a = 0; a < MR; ++a) {
+        const int i = r0 + ty + 16 * a;
+        if (i >= m) break;
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            const int j = r0 + tx + 16 * b;
+            if (j <= i) {
+                double upd = ci0[a] * lj0[b];
+                if (TWO) upd += ci1[a] * lj1[b];
+                F[i * ld + j] -= upd;
+            }
+        }
+    }
+}
+
+// generic (global-memory) Schur update, any m
+template <bool TWO>
+__device__ void schur_update_generic(double* F, int ld, int m, int k, double d0, double d1, double d2) {
+    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    const int r0 = k + (TWO ? 2 : 1);
+    for (int i = r0 + ty; i < m; i += 16) {
+        const double a0 = F[i * ld + k];
+        const double a1 = TWO ? F[i * ld + k + 1] : 0.0;
+        for (int j = r0 + tx; j <= i; j += 16) {
+            const double x0 = F[j * ld + k];
+            double upd;
+            if (TWO) {
+                const double x1 = F[j * ld + k + 1];
+                upd = a0 * (d2 * x0 - d1 * x1) + a1 * (d0 * x1 - d1 * x0);
+            } else {
+                upd = a0 * (x0 * d0);
+            }
+            F[i * ld + j] -= upd;
+        }
+    }
+}
+
+struct FrontShared {
+    PivotDecision dec;
+    int stuck;
+};
+
+// Factor one front whose lower triangle is in F (ld), fully-summed columns 0..p-1.
+// Writes L (packed trapezoid), pivot kinds, permuted row ids, CB, inertia counters.
+template <int MR>
+__device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, const FactorArgs& A, int f,
+                             FrontShared* sh) {
+    const int tid = threadIdx.x;
+    const double thres = DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits);
+    int8_t* piv = A.piv + A.rows_off[f];
+    long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
+    int k = 0;
+    while (k < p) {
+        if (tid < 64) {
+            PivotDecision d = search_pivot(F, ld, m, k, p, A.u, thres);
+            if (tid == 0) sh->dec = d;
+        }
+        __syncthreads();
+        PivotDecision d = sh->dec;
+        if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
+        if (d.c != k) {
+            sym_swap(F, ld, m, k, d.c, lrow);
+            __syncthreads();
+        }
+        if (d.kind == PIV_2X2_A) {
+            int r = d.r == k ? d.c : d.r;
+            if (r != k + 1) {
+                sym_swap(F, ld, m, k + 1, r, lrow);
+                __syncthreads();
+            }
+        }
+        if (tid == 0) {
+            if (sh->dec.kind == PIV_STUCK) nstuck++;
+            nrel += d.relaxed;
+        }
+        if (d.kind == PIV_NULL) {
+            for (int i = k + 1 + tid; i < m; i += kThreads) F[i * ld + k] = 0.0;
+            if (tid == 0) { piv[k] = PIV_NULL; nzero++; }
+            __syncthreads();
+            k += 1;
+        } else if (d.kind == PIV_1X1) {
+            const double dk = F[k * ld + k];
+            const double dinv = 1.0 / dk;
+            if (MR > 0) schur_update_tile<(MR > 0 ? MR : 1), false>(F, ld, m, k, dinv, 0.0, 0.0);
+            else schur_update_generic<false>(F, ld, m, k, dinv, 0.0, 0.0);
+            if (tid == 0) { piv[k] = PIV_1X1; if (dk > 0.0) npos++; else nneg++; }
+            __syncthreads();
+            k += 1;
+        } else {  // 2x2
+            const double a = F[k * ld + k], b = F[(k + 1) * ld + k], e = F[(k + 1) * ld + k + 1];
+            const double det = a * e - b * b;
+            const double idet = 1.0 / det;
+            if (MR > 0) schur_update_tile<(MR > 0 ? MR : 1), true>(F, ld, m, k, a * idet, b * idet, e * idet);
+            else schur_update_generic<true>(F, ld, m, k, a * idet, b * idet, e * idet);
+            if (tid == 0) {
+                piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; n2++;
+                if (det < 0.0) { npos++; nneg++; }
+                else if (a + e > 0.0) npos += 2;
+                else nneg += 2;
+            }
+            __syncthreads();
+            k += 2;
+        }
+    }
+    // ---- write L: packed lower trapezoid, column j rows j..m-1 ----
+    double* L = A.L + A.L_off[f];
+    const int64_t total = (int64_t)p * m - (int64_t)p * (p - 1) / 2;
+    {
+        int j = 0;
+        int64_t cs = 0;  // start of column j
+        for (int64_t t = tid; t < total; t += kThreads) {
+            while (t >= cs + (m - j)) { cs += m - j; ++j; }
+            const int i = j + (int)(t - cs);
+            const int8_t kind = piv[j];
+            double v;
+            if (i == j) {
+                v = kind == PIV_NULL ? 0.0 : F[j * ld + j];
+            } else if (kind == PIV_1X1) {
+                v = F[i * ld + j] / F[j * ld + j];
+            } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+                const int k0 = kind == PIV_2X2_A ? j : j - 1;
+                if (kind == PIV_2X2_A && i == j + 1) {
+                    v = F[(j + 1) * ld + j];  // D off-diagonal
+                } else {
+                    const double a = F[k0 * ld + k0], b = F[(k0 + 1) * ld + k0], e = F[(k0 + 1) * ld + k0 + 1];
+                    const double det = a * e - b * b;
+                    const double x0 = F[i * ld + k0], x1 = F[i * ld + k0 + 1];
+                    v = kind == PIV_2X2_A ? (e * x0 - b * x1) / det : (a * x1 - b * x0) / det;
+                }
+            } else {
+                v = 0.0;
+            }
+            L[t] = v;
+        }
+    }
+    // ---- permuted row ids (fully-summed part) ----
+    for (int i = tid; i < m; i += kThreads) A.frow[A.rows_off[f] + i] = lrow[i];
+    // ---- contribution block: packed lower, column-major, order cm = m - p ----
+    const int cm = m - p;
+    if (cm > 0) {
+        double* cb = A.cb + A.cb_off[f];
+        const int64_t ctot = (int64_t)cm * (cm + 1) / 2;
+        int j = 0;
+        int64_t cs = 0;
+        for (int64_t t = tid; t < ctot; t += kThreads) {
+            while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
+            const int i = j + (int)(t - cs);
+            cb[t] = F[(p + i) * ld + (p + j)];
+        }
+    }
+    if (tid == 0) {
+        atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)npos);
+        atomicAdd((unsigned long long*)&A.counters[1], (unsigned long long)nneg);
+        atomicAdd((unsigned long long*)&A.counters[2], (unsigned long long)nzero);
+        atomicAdd((unsigned long long*)&A.counters[3], (unsigned long long)n2);
+        atomicAdd((unsigned long long*)&A.counters[4], (unsigned long long)nrel);
+        atomicAdd((unsigned long long*)&A.counters[5], (unsigned long long)nstuck);
+    }
+}
+
+// assemble original entries and children contribution blocks into F (zeroed lower triangle)
+__device__ void assemble_front(double* F, int ld, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
+                               const FactorArgs& A, int f) {
+    const int tid = threadIdx.x;
+    const int64_t ro = A.rows_off[f];
+    for (int i = tid; i < m; i += kThreads) {
+        const int32_t v = A.rows[ro + i];
+        lrow[i] = v;
+        sloc[i] = A.scale[v];
+    }
+    for (int i = tid; i < m; i += kThreads) {
+        double* Fi = F + (int64_t)i * ld;
+        for (int j = 0; j <= i; ++j) Fi[j] = 0.0;
+    }
+    __syncthreads();
+    for (int64_t e = A.ent_off[f] + tid; e < A.ent_off[f + 1]; e += kThreads) {
+        const uint32_t lp = A.ent_lpos[e];
+        const int lr = (int)(lp >> 16), lc = (int)(lp & 0xffffu);
+        F[lr * ld + lc] = sloc[lr] * A.uval[e] * sloc[lc];
+    }
+    for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
+        const int c = A.child[ci];
+        const int cm = A.fm[c] - A.fp[c];
+        if (cm <= 0) continue;
+        __syncthreads();  // previous child's adds done, rstage free
+        const int32_t* rm = A.relmap + A.relmap_off[c];
+        for (int i = tid; i < cm; i += kThreads) rstage[i] = rm[i];
+        __syncthreads();
+        const double* cb = A.cb + A.cb_off[c];
+        const int64_t ctot = (int64_t)cm * (cm + 1) / 2;
+        int j = 0;
+        int64_t cs = 0;
+        for (int64_t t = tid; t < ctot; t += kThreads) {
+            while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
+            const int i = j + (int)(t - cs);
+            F[rstage[i] * ld + rstage[j]] += cb[t];
+        }
+    }
+    __syncthreads();
+}
+
+template <int MR>
+__global__ __launch_bounds__(kThreads) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int ld = m | 1;
+    double* F = smem + 4;
+    double* sloc = F + (int64_t)ld * m;
+    int32_t* lrow = (int32_t*)(sloc + m);
+    int32_t* rstage = lrow + m;
+    assemble_front(F, ld, m, p, lrow, sloc, rstage, A, f);
+    factor_front<MR>(F, ld, m, p, lrow, A, f, sh);
+}
+
+__global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int ld = m;
+    double* F = A.gscratch + A.gscratch_off[f];
+    double* sloc = smem + 4;
+    int32_t* lrow = (int32_t*)(sloc + m);
+    int32_t* rstage = lrow + m;
+    assemble_front(F, ld, m, p, lrow, sloc, rstage, A, f);
+    factor_front<0>(F, ld, m, p, lrow, A, f, sh);
+}
+
+// ------------------------------------------------------------------------------------------------
+// triangular solves (multifrontal, level by level)
+// ------------------------------------------------------------------------------------------------
+
+__device__ __forceinline__ int64_t colptr(int64_t L_off, int m, int k) {
+    return L_off + (int64_t)k * m - (int64_t)k * (k - 1) / 2 - k;  // L(i,k) = L[colptr + i], i >= k
+}
+
+__global__ void k_rhs_scale(const double* __restrict__ b, const double* __restrict__ scale, double* __restrict__ w,
+                            int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        w[i] = scale[i] * b[i];
+}
+
+__global__ void k_unscale(const double* __restrict__ w, const double* __restrict__ scale, double* __restrict__ x,
+                          int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = scale[i] * w[i];
+}
+
+__global__ __launch_bounds__(kThreads) void k_solve_fwd(SolveArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double y[];
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int tid = threadIdx.x;
+    const int64_t ro = A.rows_off[f];
+    const int8_t* piv = A.piv + ro;
+    for (int i = tid; i < m; i += kThreads) y[i] = i < p ? A.w[A.frow[ro + i]] : 0.0;
+    for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
+        const int c = A.child[ci];
+        const int cm = A.fm[c] - A.fp[c];
+        __syncthreads();
+        const int32_t* rm = A.relmap + A.relmap_off[c];
+        const double* cv = A.cvec + A.relmap_off[c];
+        for (int t = tid; t < cm; t += kThreads) y[rm[t]] += cv[t];
+    }
+    __syncthreads();
+    const int64_t Lo = A.L_off[f];
+    for (int k = 0; k < p; ++k) {
+        const int8_t kind = piv[k];
+        if (kind == PIV_1X1) {
+            const double yk = y[k];
+            const double* Lk = A.L + colptr(Lo, m, k);
+            for (int i = k + 1 + tid; i < m; i += kThreads) y[i] -= Lk[i] * yk;
+        } else if (kind == PIV_2X2_A) {
+            const double y0 = y[k], y1 = y[k + 1];
+            const double* L0 = A.L + colptr(Lo, m, k);
+            const double* L1 = A.L + colptr(Lo, m, k + 1);
+            for (int i = k + 2 + tid; i < m; i += kThreads) y[i] -= L0[i] * y0 + L1[i] * y1;
+            ++k;
+        }
+        __syncthreads();
+    }
+    // block diagonal
+    for (int k = tid; k < p; k += kThreads) {
+        const int8_t kind = piv[k];
+        double z;
+        if (kind == PIV_1X1) {
+            z = y[k] / A.L[colptr(Lo, m, k) + k];
+            A.w[A.frow[ro + k]] = z;
+        } else if (kind == PIV_2X2_A) {
+            const double a = A.L[colptr(Lo, m, k) + k], b = A.L[colptr(Lo, m, k) + k + 1];
+            const double e = A.L[colptr(Lo, m, k + 1) + k + 1];
+            const double det = a * e - b * b;
+            const double y0 = y[k], y1 = y[k + 1];
+            A.w[A.frow[ro + k]] = (e * y0 - b * y1) / det;
+            A.w[A.frow[ro + k + 1]] = (a * y1 - b * y0) / det;
+        } else if (kind != PIV_2X2_B) {
+            A.w[A.frow[ro + k]] = 0.0;  // null pivot contributes 0
+        }
+    }
+    double* cv = A.cvec + A.relmap_off[f];
+    for (int i = p + tid; i < m; i += kThreads) cv[i - p] = y[i];
+}
+
+__global__ __launch_bounds__(kThreads) void k_solve_bwd(SolveArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double x[];
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int64_t ro = A.rows_off[f];
+    const int8_t* piv = A.piv + ro;
+    const int64_t Lo = A.L_off[f];
+    for (int i = tid; i < m; i += kThreads) x[i] = A.w[A.frow[ro + i]];
+    __syncthreads();
+    // rectangular part: x_k -= sum_{i>=p} L(i,k) x_i, one wave per column
+    for (int k = wave; k < p; k += kThreads / 64) {
+        const double* Lk = A.L + colptr(Lo, m, k);
+        double s = 0.0;
+        for (int i = p + lane; i < m; i += 64) s += Lk[i] * x[i];
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+        if (lane == 0 && piv[k] != PIV_NULL) x[k] -= s;
+    }
+    __syncthreads();
+    // triangle, column sweep from the last pivot
+    for (int k = p - 1; k >= 0; --k) {
+        const int8_t kind = piv[k];
+        if (kind != PIV_NULL) {
+            const double xk = x[k];
+            const int skip = kind == PIV_2X2_B ? k - 1 : -1;
+            for (int j = tid; j < k; j += kThreads)
+                if (j != skip && piv[j] != PIV_NULL) x[j] -= A.L[colptr(Lo, m, j) + k] * xk;
+        }
+        __syncthreads();
+    }
+    for (int k = tid; k < p; k += kThreads) A.w[A.frow[ro + k]] = x[k];
+}
+
+// ------------------------------------------------------------------------------------------------
+// host-side launch helpers
+// ------------------------------------------------------------------------------------------------
+
+static int grid_for(int64_t n, int block) {
+    int64_t g = (n + block - 1) / block;
+    if (g > 4096) g = 4096;
+    if (g < 1) g = 1;
+    return (int)g;
+}
+
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* ent_r,
+                       const int32_t* ent_c, int64_t nu, double* uval, unsigned long long* rmax, hipStream_t s) {
+    if (nu == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(nu, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, ent_r, ent_c, nu,
+                       uval, rmax);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale(const double* uval, const int32_t* ent_r, const int32_t* ent_c, int64_t nu, int64_t n,
+                        int iters, double* scale, unsigned long long* rmax, double* rowsum,
+                        unsigned long long* anorm, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    for (int it = 0; it < iters; ++it) {
+        if (it > 0) {
+            hipMemsetAsync(rmax, 0, sizeof(unsigned long long) * n, s);
+            hipLaunchKernelGGL(k_rowmax_scaled, dim3(grid_for(nu, 256)), dim3(256), 0, s, uval, ent_r, ent_c, scale,
+                               nu, rmax);
+        }
+        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(n, 256)), dim3(256), 0, s, rmax, scale, n, it == 0 ? 1 : 0);
+    }
+    if (iters == 0) {  // no scaling: s = 1
+        hipMemsetAsync(rmax, 0, sizeof(unsigned long long) * n, s);
+        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(n, 256)), dim3(256), 0, s, rmax, scale, n, 1);
+    }
+    if (nu > 0)
+        hipLaunchKernelGGL(k_rowsum, dim3(grid_for(nu, 256)), dim3(256), 0, s, uval, ent_r, ent_c, scale, nu, rowsum);
+    hipLaunchKernelGGL(k_normmax, dim3(grid_for(n, kThreads) > 1024 ? 1024 : grid_for(n, kThreads)), dim3(kThreads), 0,
+                       s, rowsum, n, anorm);
+    return hipGetLastError();
+}
+
+size_t factor_lds_bytes(int mmax) {
+    int ld = mmax | 1;
+    return 32 + (size_t)ld * mmax * sizeof(double) + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t);
+}
+
+hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    if (global) {
+        size_t sh = 32 + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t);
+        hipLaunchKernelGGL(k_factor_global, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    } else {
+        size_t sh = factor_lds_bytes(mmax);
+        if (mmax <= 32) hipLaunchKernelGGL(k_factor_lds<2>, dim3(count), dim3(kThreads), sh, s, A, fronts);
+        else if (mmax <= 64) hipLaunchKernelGGL(k_factor_lds<4>, dim3(count), dim3(kThreads), sh, s, A, fronts);
+        else hipLaunchKernelGGL(k_factor_lds<8>, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rhs_scale, dim3(grid_for(n, 256)), dim3(256), 0, s, b, scale, w, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s) {
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unscale, dim3(grid_for(n, 256)), dim3(256), 0, s, w, scale, x, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, bool forward, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    size_t sh = (size_t)mmax * sizeof(double) + 16;
+    if (forward) hipLaunchKernelGGL(k_solve_fwd, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    else hipLaunchKernelGGL(k_solve_bwd, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    return hipGetLastError();
+}
+
+}  // namespace ukkt

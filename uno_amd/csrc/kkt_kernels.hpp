@@ -1,0 +1,68 @@
+// kkt_kernels.hpp -- device-argument structs and launch wrappers of kkt_kernels.hip.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ukkt {
+
+// Arguments of the front factorization kernels (device pointers, SoA per front).
+struct FactorArgs {
+    const int32_t* fm;          // front order
+    const int32_t* fp;          // fully-summed columns
+    const int64_t* rows_off;    // nf+1
+    const int32_t* rows;        // original ids, analysis order
+    const int64_t* ent_off;     // nf+1 packed slot ranges
+    const uint32_t* ent_lpos;   // (lr << 16) | lc
+    const double* uval;         // packed summed values
+    const double* scale;        // equilibration, by original id
+    const int32_t* child_off;   // nf+1
+    const int32_t* child;
+    const int64_t* relmap_off;  // per front: cb rows into relmap / cvec
+    const int32_t* relmap;
+    const int64_t* L_off;
+    const int64_t* cb_off;
+    const int64_t* gscratch_off;  // per front, only used by k_factor_global
+    const unsigned long long* anorm_bits;
+    double* L;
+    double* cb;
+    double* gscratch;
+    int32_t* frow;              // row ids after pivoting (same layout as rows)
+    int8_t* piv;                // pivot kinds (same layout as rows)
+    unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck
+    double u;
+    double null_fac;
+};
+
+struct SolveArgs {
+    const int32_t* fm;
+    const int32_t* fp;
+    const int64_t* rows_off;
+    const int32_t* frow;
+    const int8_t* piv;
+    const int32_t* child_off;
+    const int32_t* child;
+    const int64_t* relmap_off;
+    const int32_t* relmap;
+    const int64_t* L_off;
+    const double* L;
+    double* w;      // work vector by original id (scaled space)
+    double* cvec;   // per-front update vectors (layout of relmap)
+};
+
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* ent_r,
+                       const int32_t* ent_c, int64_t nu, double* uval, unsigned long long* rmax, hipStream_t s);
+hipError_t launch_scale(const double* uval, const int32_t* ent_r, const int32_t* ent_c, int64_t nu, int64_t n,
+                        int iters, double* scale, unsigned long long* rmax, double* rowsum,
+                        unsigned long long* anorm, hipStream_t s);
+size_t factor_lds_bytes(int mmax);
+hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
+hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
+hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
+hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, bool forward, hipStream_t s);
+
+constexpr int kMaxLdsFront = 128;     // fronts up to this order factor entirely in LDS
+constexpr int kMaxGlobalFront = 8192; // larger fronts are rejected at analysis
+
+}  // namespace ukkt

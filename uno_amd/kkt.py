@@ -1,0 +1,394 @@
+"""ctypes binding of the MI355X KKT backend (uno_amd/libuno_kkt.so, C ABI in include/uno_kkt.h).
+
+This is the Python-side mirror of Uno's linear-solver plugin surface, used by the tests and by
+bench.py; the production drop-in is the C++ adapter in integration/ (see INTEGRATION.md).  Method
+names follow uno/ingredients/subproblem_solvers/DirectSymmetricIndefiniteLinearSolver.hpp:11-25 and
+uno/ingredients/subproblem_solvers/SymmetricIndefiniteLinearSolver.hpp:20-33.
+
+There is no CPU fallback: if the HIP library is missing or no GPU is visible, every call raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libuno_kkt.so")
+GEN_PATH = os.path.join(_HERE, "libarrowband.so")
+
+UNO_KKT_OK = 0
+_ERR_NAMES = {-1: "ERR_ARG", -2: "ERR_STATE", -3: "ERR_HIP", -4: "ERR_PIVOT", -5: "ERR_NOMEM", -6: "ERR_NODEVICE"}
+
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_f64p = ctypes.POINTER(ctypes.c_double)
+
+
+class KKTStats(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64), ("nnz", ctypes.c_int64), ("nnz_unique", ctypes.c_int64), ("nnz_L", ctypes.c_int64),
+        ("n_fronts", ctypes.c_int64), ("n_levels", ctypes.c_int64), ("max_front", ctypes.c_int64),
+        ("n_dense", ctypes.c_int64), ("pivots_2x2", ctypes.c_int64), ("pivots_null", ctypes.c_int64),
+        ("pivots_relaxed", ctypes.c_int64), ("factorizations", ctypes.c_int64), ("solves", ctypes.c_int64),
+        ("flops", ctypes.c_double), ("analysis_seconds", ctypes.c_double), ("bytes_L", ctypes.c_double),
+        ("bytes_cb", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+EXPORTED_SYMBOLS = [
+    "uno_kkt_create", "uno_kkt_destroy", "uno_kkt_set_option", "uno_kkt_analyze", "uno_kkt_factorize",
+    "uno_kkt_set_values", "uno_kkt_fill_values", "uno_kkt_inertia", "uno_kkt_solve", "uno_kkt_stats",
+    "uno_kkt_kernel_times", "uno_kkt_reset_kernel_times", "uno_kkt_stream", "uno_kkt_last_error",
+    "uno_kkt_version",
+]
+
+_lib = None
+
+
+def load_library():
+    """Load libuno_kkt.so (raises if it was not built: no silent fallback)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RuntimeError(f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(LIB_PATH)
+    vp = ctypes.c_void_p
+    lib.uno_kkt_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    lib.uno_kkt_destroy.argtypes = [vp]
+    lib.uno_kkt_destroy.restype = None
+    lib.uno_kkt_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_double]
+    lib.uno_kkt_analyze.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p]
+    lib.uno_kkt_factorize.argtypes = [vp, ctypes.c_void_p, ctypes.c_int]
+    lib.uno_kkt_set_values.argtypes = [vp, _i64p, _f64p, ctypes.c_int64]
+    lib.uno_kkt_fill_values.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_double]
+    lib.uno_kkt_inertia.argtypes = [vp, _i64p, _i64p, _i64p]
+    lib.uno_kkt_solve.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]
+    lib.uno_kkt_stats.argtypes = [vp, ctypes.POINTER(KKTStats)]
+    lib.uno_kkt_kernel_times.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, _f64p, _i64p, ctypes.c_int]
+    lib.uno_kkt_reset_kernel_times.argtypes = [vp]
+    lib.uno_kkt_stream.argtypes = [vp]
+    lib.uno_kkt_stream.restype = ctypes.c_void_p
+    lib.uno_kkt_last_error.argtypes = [vp]
+    lib.uno_kkt_last_error.restype = ctypes.c_char_p
+    lib.uno_kkt_version.restype = ctypes.c_char_p
+    _lib = lib
+    return lib
+
+
+class KKTError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__(f"uno_kkt {_ERR_NAMES.get(code, code)}: {msg}")
+        self.code = code
+
+
+def _i64(a):
+    a = np.ascontiguousarray(a, dtype=np.int64)
+    return a, a.ctypes.data_as(_i64p)
+
+
+def _f64(a):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    return a, a.ctypes.data_as(_f64p)
+
+
+class HipKKT:
+    """Thin object over one uno_kkt handle (analyze / factorize / inertia / solve)."""
+
+    def __init__(self, device=0, **options):
+        self.lib = load_library()
+        h = ctypes.c_void_p()
+        rc = self.lib.uno_kkt_create(ctypes.byref(h), int(device))
+        if rc != UNO_KKT_OK:
+            raise KKTError(rc, "uno_kkt_create failed (no HIP device?)")
+        self.h = h
+        self.n = 0
+        for k, v in options.items():
+            self.set_option(k, v)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.uno_kkt_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        self.close()
+
+    def _check(self, rc):
+        if rc != UNO_KKT_OK:
+            raise KKTError(rc, self.lib.uno_kkt_last_error(self.h).decode())
+
+    def set_option(self, name, value):
+        self._check(self.lib.uno_kkt_set_option(self.h, name.encode(), float(value)))
+
+    def analyze(self, n, rows, cols):
+        r, rp = _i64(rows)
+        c, cp = _i64(cols)
+        if len(r) != len(c):
+            raise ValueError("rows and cols differ in length")
+        self.n = int(n)
+        self._check(self.lib.uno_kkt_analyze(self.h, self.n, len(r), rp, cp))
+
+    def factorize(self, values=None, device_ptr=None):
+        """values: host array (COO order), or device_ptr (int address), or neither (reuse)."""
+        if device_ptr is not None:
+            self._check(self.lib.uno_kkt_factorize(self.h, ctypes.c_void_p(int(device_ptr)), 1))
+        elif values is not None:
+            v, vp = _f64(values)
+            self._v_keep = v
+            self._check(self.lib.uno_kkt_factorize(self.h, v.ctypes.data_as(ctypes.c_void_p), 0))
+        else:
+            self._check(self.lib.uno_kkt_factorize(self.h, None, 0))
+
+    def fill_values(self, first, count, value):
+        self._check(self.lib.uno_kkt_fill_values(self.h, int(first), int(count), float(value)))
+
+    def set_values(self, positions, values):
+        p, pp = _i64(positions)
+        v, vp = _f64(values)
+        self._check(self.lib.uno_kkt_set_values(self.h, pp, vp, len(p)))
+
+    def inertia(self):
+        p, q, z = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
+        self._check(self.lib.uno_kkt_inertia(self.h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(z)))
+        return (p.value, q.value, z.value)
+
+    def solve(self, rhs):
+        b, _ = _f64(rhs)
+        x = np.zeros(self.n, dtype=np.float64)
+        self._check(self.lib.uno_kkt_solve(self.h, b.ctypes.data_as(ctypes.c_void_p),
+                                           x.ctypes.data_as(ctypes.c_void_p), 0))
+        return x
+
+    def solve_device(self, rhs_ptr, x_ptr):
+        self._check(self.lib.uno_kkt_solve(self.h, ctypes.c_void_p(int(rhs_ptr)), ctypes.c_void_p(int(x_ptr)), 1))
+
+    def stats(self):
+        s = KKTStats()
+        self._check(self.lib.uno_kkt_stats(self.h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def stream(self):
+        return self.lib.uno_kkt_stream(self.h)
+
+    def kernel_times(self):
+        names = ctypes.create_string_buffer(512)
+        ms = np.zeros(16, dtype=np.float64)
+        cnt = np.zeros(16, dtype=np.int64)
+        k = self.lib.uno_kkt_kernel_times(self.h, names, 512, ms.ctypes.data_as(_f64p), cnt.ctypes.data_as(_i64p), 16)
+        keys = names.value.decode().split(",")
+        return {keys[i]: (float(ms[i]), int(cnt[i])) for i in range(k)}
+
+    def reset_kernel_times(self):
+        self._check(self.lib.uno_kkt_reset_kernel_times(self.h))
+
+
+# ---------------------------------------------------------------------------------------------
+# Uno plugin-surface mirror (names as in the reference)
+# ---------------------------------------------------------------------------------------------
+
+class SparseSymmetricMatrix:
+    """Mirror of SparseSymmetricMatrix<COOFormat<size_t,double>> (uno/linear_algebra/COOFormat.hpp:19-141):
+    regularization diagonal inserted first by reset(), insert() appends, set_regularization()
+    overwrites entries[index + offset], duplicates kept (summed by the solver)."""
+
+    def __init__(self, dimension, capacity, regularization_size):
+        self._dimension = int(dimension)
+        self.regularization_size = int(regularization_size)
+        self.capacity = int(capacity) + self.regularization_size
+        self.reset()
+
+    def reset(self):
+        r = self.regularization_size
+        self.rows = list(range(r))
+        self.cols = list(range(r))
+        self.entries = [0.0] * r
+
+    def dimension(self):
+        return self._dimension
+
+    def number_nonzeros(self):
+        return len(self.entries)
+
+    def insert(self, row_index, column_index, term):
+        self.rows.append(int(row_index))
+        self.cols.append(int(column_index))
+        self.entries.append(float(term))
+
+    def finalize_column(self, column_index):
+        pass
+
+    def set_regularization(self, indices, offset, factor):
+        for i in indices:
+            self.entries[i + offset] = float(factor)
+
+    def smallest_diagonal_entry(self, max_dimension):
+        d = np.zeros(max_dimension)
+        for r, c, v in zip(self.rows, self.cols, self.entries):
+            if r == c and r < max_dimension:
+                d[r] += v
+        return float(d.min())
+
+    def arrays(self):
+        return (np.asarray(self.rows, dtype=np.int64), np.asarray(self.cols, dtype=np.int64),
+                np.asarray(self.entries, dtype=np.float64))
+
+    def product(self, x):
+        """SymmetricMatrix::product (uno/linear_algebra/SymmetricMatrix.hpp:100-109)."""
+        r, c, v = self.arrays()
+        y = np.zeros(self._dimension)
+        np.add.at(y, r, v * x[c])
+        off = r != c
+        np.add.at(y, c[off], v[off] * x[r[off]])
+        return y
+
+
+class HipLDLSolver:
+    """Mirror of DirectSymmetricIndefiniteLinearSolver<size_t,double> backed by the GPU
+    (the C++ adapter integration/HIPLDLSolver.cpp is the production form)."""
+
+    def __init__(self, device=0, **options):
+        self.kkt = HipKKT(device, **options)
+        self.dimension = 0
+
+    def initialize_memory(self, number_variables, number_constraints, number_hessian_nonzeros, regularization_size):
+        self.dimension = number_variables + number_constraints
+
+    def do_symbolic_analysis(self, matrix):
+        r, c, _ = matrix.arrays()
+        self.kkt.analyze(matrix.dimension(), r, c)
+
+    def do_numerical_factorization(self, matrix):
+        self.kkt.factorize(matrix.arrays()[2])
+
+    def solve_indefinite_system(self, matrix, rhs, result=None):
+        x = self.kkt.solve(np.asarray(rhs, dtype=np.float64))
+        if result is not None:
+            result[:] = x
+        return x
+
+    def get_inertia(self):
+        return self.kkt.inertia()
+
+    def number_negative_eigenvalues(self):
+        return self.kkt.inertia()[1]
+
+    def number_zero_eigenvalues(self):
+        return self.kkt.inertia()[2]
+
+    def matrix_is_singular(self):
+        return self.number_zero_eigenvalues() > 0
+
+    def rank(self):
+        return self.kkt.n - self.number_zero_eigenvalues()
+
+
+class UnstableRegularization(RuntimeError):
+    """uno/ingredients/regularization_strategies/UnstableRegularization.hpp:10-15"""
+
+
+def regularize_augmented_matrix(matrix, primal_indices, dual_indices, dual_regularization_parameter,
+                                expected_inertia, linear_solver, state, options=None, trace=None):
+    """Mirror of PrimalDualRegularization::regularize_augmented_matrix
+    (uno/ingredients/regularization_strategies/PrimalDualRegularization.hpp:133-219) with the
+    default option values (uno/options/DefaultOptions.cpp).  `state` carries
+    previous_primal_regularization and symbolic_analysis_performed across calls."""
+    o = dict(regularization_failure_threshold=1e40, primal_regularization_initial_factor=1e-4,
+             dual_regularization_fraction=1e-8, primal_regularization_lb=1e-20,
+             primal_regularization_decrease_factor=3.0, primal_regularization_fast_increase_factor=100.0,
+             primal_regularization_slow_increase_factor=8.0, threshold_unsuccessful_attempts=8)
+    if options:
+        o.update(options)
+    primal, dual = 0.0, 0.0
+    attempts = 1
+    if not state.get("symbolic_analysis_performed"):
+        linear_solver.do_symbolic_analysis(matrix)
+        state["symbolic_analysis_performed"] = True
+    linear_solver.do_numerical_factorization(matrix)
+    inertia = tuple(linear_solver.get_inertia())
+    if trace is not None:
+        trace.append((primal, dual, inertia))
+    if inertia == tuple(expected_inertia):
+        return primal, dual, attempts
+    if linear_solver.matrix_is_singular():
+        dual = o["dual_regularization_fraction"] * dual_regularization_parameter
+    prev = state.get("previous_primal_regularization", 0.0)
+    if prev == 0.0:
+        primal = o["primal_regularization_initial_factor"]
+    else:
+        primal = max(o["primal_regularization_lb"], prev / o["primal_regularization_decrease_factor"])
+    matrix.set_regularization(primal_indices, 0, primal)
+    matrix.set_regularization(dual_indices, len(primal_indices), -dual)
+    while True:
+        linear_solver.do_numerical_factorization(matrix)
+        attempts += 1
+        inertia = tuple(linear_solver.get_inertia())
+        if trace is not None:
+            trace.append((primal, dual, inertia))
+        if inertia == tuple(expected_inertia):
+            state["previous_primal_regularization"] = primal
+            return primal, dual, attempts
+        if prev == 0.0 or o["threshold_unsuccessful_attempts"] < attempts:
+            primal *= o["primal_regularization_fast_increase_factor"]
+        else:
+            primal *= o["primal_regularization_slow_increase_factor"]
+        if primal <= o["regularization_failure_threshold"]:
+            matrix.set_regularization(primal_indices, 0, primal)
+            matrix.set_regularization(dual_indices, len(primal_indices), -dual)
+        else:
+            raise UnstableRegularization()
+
+
+# ---------------------------------------------------------------------------------------------
+# synthetic inputs
+# ---------------------------------------------------------------------------------------------
+
+_gen = None
+
+SEEDS = {"C2": 0x5EED0002, "C3": 0x5EED0003, "C5": 0x5EED0005}
+
+
+def _load_gen():
+    global _gen
+    if _gen is None:
+        if not os.path.exists(GEN_PATH):
+            raise RuntimeError(f"{GEN_PATH} not built")
+        g = ctypes.CDLL(GEN_PATH)
+        g.arrowband_size.argtypes = [ctypes.c_int64, _i64p, _i64p]
+        g.arrowband_size.restype = ctypes.c_int64
+        g.arrowband_generate.argtypes = [ctypes.c_int64, ctypes.c_uint64, _i64p, _i64p, _f64p]
+        g.arrowband_generate.restype = ctypes.c_int64
+        g.arrowband_rhs.argtypes = [ctypes.c_int64, ctypes.c_uint64, _f64p]
+        g.coo_symv.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, _f64p, _f64p, _f64p]
+        _gen = g
+    return _gen
+
+
+def arrowband(N, seed):
+    """Return (n, nv, m, rows, cols, vals, rhs) of the arrowband KKT of dimension N."""
+    g = _load_gen()
+    nv, m = ctypes.c_int64(), ctypes.c_int64()
+    nnz = g.arrowband_size(int(N), ctypes.byref(nv), ctypes.byref(m))
+    rows = np.empty(nnz, dtype=np.int64)
+    cols = np.empty(nnz, dtype=np.int64)
+    vals = np.empty(nnz, dtype=np.float64)
+    got = g.arrowband_generate(int(N), int(seed), rows.ctypes.data_as(_i64p), cols.ctypes.data_as(_i64p),
+                               vals.ctypes.data_as(_f64p))
+    if got != nnz:
+        raise ValueError(f"arrowband generation failed for N={N}")
+    rhs = np.empty(int(N), dtype=np.float64)
+    g.arrowband_rhs(int(N), int(seed), rhs.ctypes.data_as(_f64p))
+    return int(N), nv.value, m.value, rows, cols, vals, rhs
+
+
+def coo_symv(n, rows, cols, vals, x):
+    g = _load_gen()
+    r, rp = _i64(rows)
+    c, cp = _i64(cols)
+    v, vp = _f64(vals)
+    xx, xp = _f64(x)
+    y = np.zeros(int(n), dtype=np.float64)
+    g.coo_symv(int(n), len(r), rp, cp, vp, xp, y.ctypes.data_as(_f64p))
+    return y
