@@ -51,6 +51,7 @@ typedef struct {
     double analysis_seconds;/* host wall time of the last uno_kkt_analyze */
     double bytes_L;         /* 8 * stored factor entries (L + D) */
     double bytes_cb;        /* 8 * contribution-block entries written per factorization */
+    int64_t fronts_merged;  /* fronts amalgamated into their parent since analysis (delayed pivots) */
 } uno_kkt_stats_t;
 
 /* Create a solver bound to HIP device `device_id`.  Replaces MUMPS JOB=-1 (MUMPSSolver.cpp:16-37). */

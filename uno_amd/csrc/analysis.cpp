@@ -170,16 +170,16 @@ private:
 
 }  // namespace
 
-std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
-                    const AnalysisOptions& opt, Symbolic& S) {
-    S = Symbolic();
+std::string order_pattern(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
+                          const AnalysisOptions& opt, Pattern& P) {
+    P = Pattern();
     if (n < 0 || nnz < 0) return "negative size";
     if (n >= (int64_t(1) << 31) - 1 || nnz >= (int64_t(1) << 31) - 1) return "n or nnz exceeds int32 range";
     for (int64_t k = 0; k < nnz; ++k)
         if (row[k] < 0 || row[k] >= n || col[k] < 0 || col[k] >= n)
             return "COO entry " + std::to_string(k) + " out of range";
-    S.n = n;
-    S.nnz = nnz;
+    P.n = n;
+    P.nnz = nnz;
     const int32_t N = (int32_t)n;
 
     // ---- canonical lower pattern: bucket by min index, sort by (max index, position) ----
@@ -194,68 +194,84 @@ std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* c
             pr[fill[b]++] = {(int32_t)a, (int32_t)k};
         }
     }
-    std::vector<int32_t> ur, uc, udp;  // unique rows/cols, first position in pr
-    ur.reserve(nnz);
-    uc.reserve(nnz);
-    udp.reserve(nnz + 1);
+    P.ur.reserve(nnz);
+    P.uc.reserve(nnz);
+    P.udp.reserve(nnz + 1);
+    P.pos_sorted.resize(nnz);
     for (int64_t b = 0; b < n; ++b) {
         auto first = pr.begin() + bstart[b], last = pr.begin() + bstart[b + 1];
         if (last - first > 1) std::sort(first, last);
         for (auto it = first; it != last; ++it) {
             if (it == first || it->first != (it - 1)->first) {
-                ur.push_back(it->first);
-                uc.push_back((int32_t)b);
-                udp.push_back((int32_t)(it - pr.begin()));
+                P.ur.push_back(it->first);
+                P.uc.push_back((int32_t)b);
+                P.udp.push_back((int32_t)(it - pr.begin()));
             }
+            P.pos_sorted[it - pr.begin()] = it->second;
         }
     }
-    const int64_t nu = (int64_t)ur.size();
-    udp.push_back((int32_t)nnz);
-    S.nu = nu;
+    P.nu = (int64_t)P.ur.size();
+    P.udp.push_back((int32_t)nnz);
+    const int64_t nu = P.nu;
 
     // ---- adjacency (no diagonal) ----
+    P.ap.assign(n + 1, 0);
+    for (int64_t u = 0; u < nu; ++u)
+        if (P.ur[u] != P.uc[u]) { P.ap[P.ur[u] + 1]++; P.ap[P.uc[u] + 1]++; }
+    for (int64_t i = 0; i < n; ++i) P.ap[i + 1] += P.ap[i];
+    P.ai.resize(P.ap[n]);
+    {
+        std::vector<int64_t> pos(P.ap.begin(), P.ap.end() - 1);
+        for (int64_t u = 0; u < nu; ++u)
+            if (P.ur[u] != P.uc[u]) { P.ai[pos[P.ur[u]]++] = P.uc[u]; P.ai[pos[P.uc[u]]++] = P.ur[u]; }
+    }
     Graph g;
     g.n = N;
-    g.ap.assign(n + 1, 0);
-    for (int64_t u = 0; u < nu; ++u)
-        if (ur[u] != uc[u]) { g.ap[ur[u] + 1]++; g.ap[uc[u] + 1]++; }
-    for (int64_t i = 0; i < n; ++i) g.ap[i + 1] += g.ap[i];
-    g.ai.resize(g.ap[n]);
-    {
-        std::vector<int64_t> pos(g.ap.begin(), g.ap.end() - 1);
-        for (int64_t u = 0; u < nu; ++u)
-            if (ur[u] != uc[u]) { g.ai[pos[ur[u]]++] = uc[u]; g.ai[pos[uc[u]]++] = ur[u]; }
-    }
+    g.ap.swap(P.ap);
+    g.ai.swap(P.ai);
 
     // ---- ordering: dense nodes last, nested dissection on the rest ----
     std::vector<char> dense(n, 0);
     const double dthr = std::max(16.0, opt.dense_factor * std::sqrt((double)n));
     for (int32_t v = 0; v < N; ++v)
-        if ((double)(g.ap[v + 1] - g.ap[v]) > dthr) { dense[v] = 1; S.n_dense++; }
+        if ((double)(g.ap[v + 1] - g.ap[v]) > dthr) { dense[v] = 1; P.n_dense++; }
     std::vector<int32_t> order;
     order.reserve(n);
     std::vector<int32_t> group_start;
     Dissector(g, dense, std::max(1, opt.leaf_size)).run(order, group_start);
-    if (S.n_dense) {
+    if (P.n_dense) {
         group_start.push_back((int32_t)order.size());
         for (int32_t v = 0; v < N; ++v) if (dense[v]) order.push_back(v);
     }
+    g.ap.swap(P.ap);
+    g.ai.swap(P.ai);
     if ((int64_t)order.size() != n) return "internal: ordering is not a permutation";
     group_start.push_back(N);
-    S.perm = order;
-    S.iperm.assign(n, -1);
-    for (int32_t q = 0; q < N; ++q) S.iperm[S.perm[q]] = q;
+    P.perm.swap(order);
 
     // ---- supernodes: each group cut into blocks of at most max_block columns ----
-    std::vector<int32_t> bfirst;
     for (size_t gi = 0; gi + 1 < group_start.size(); ++gi) {
         int32_t s = group_start[gi], e = group_start[gi + 1];
         int32_t len = e - s;
         if (len <= 0) continue;
         int32_t nb = (len + opt.max_block - 1) / opt.max_block;
-        for (int32_t b = 0; b < nb; ++b) bfirst.push_back(s + (int32_t)((int64_t)len * b / nb));
+        for (int32_t b = 0; b < nb; ++b) P.bfirst.push_back(s + (int32_t)((int64_t)len * b / nb));
     }
-    bfirst.push_back(N);
+    P.bfirst.push_back(N);
+    return "";
+}
+
+std::string build_structure(const Pattern& P, Symbolic& S) {
+    S = Symbolic();
+    const int64_t n = P.n, nnz = P.nnz, nu = P.nu;
+    S.n = n;
+    S.nnz = nnz;
+    S.nu = nu;
+    S.n_dense = P.n_dense;
+    S.perm = P.perm;
+    S.iperm.assign(n, -1);
+    for (int32_t q = 0; q < (int32_t)n; ++q) S.iperm[S.perm[q]] = q;
+    const std::vector<int32_t>& bfirst = P.bfirst;
     const int32_t nf = (int32_t)bfirst.size() - 1;
     S.nf = nf;
     std::vector<int32_t> blk(n);
@@ -275,8 +291,8 @@ std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* c
             buf.clear();
             for (int32_t j = first; j <= last; ++j) {
                 int32_t v = S.perm[j];
-                for (int64_t p = g.ap[v]; p < g.ap[v + 1]; ++p) {
-                    int32_t i = S.iperm[g.ai[p]];
+                for (int64_t p = P.ap[v]; p < P.ap[v + 1]; ++p) {
+                    int32_t i = S.iperm[P.ai[p]];
                     if (i > last && mark[i] != b) { mark[i] = b; buf.push_back(i); }
                 }
             }
@@ -360,7 +376,7 @@ std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* c
     S.f_ent_off.assign(nf + 1, 0);
     std::vector<int32_t> ublk(nu);
     for (int64_t u = 0; u < nu; ++u) {
-        int32_t a = S.iperm[ur[u]], c = S.iperm[uc[u]];
+        int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
         ublk[u] = blk[std::min(a, c)];
         S.f_ent_off[ublk[u] + 1]++;
     }
@@ -377,7 +393,7 @@ std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* c
         for (int64_t u = 0; u < nu; ++u) slot_of[u] = (int32_t)fill[ublk[u]]++;
         for (int64_t u = 0; u < nu; ++u) {
             int32_t s = slot_of[u], b = ublk[u];
-            int32_t a = S.iperm[ur[u]], c = S.iperm[uc[u]];
+            int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
             int32_t hi = std::max(a, c), lo = std::min(a, c);
             int32_t lc = lo - bfirst[b];
             int32_t lr = local_row(b, hi);
@@ -385,15 +401,15 @@ std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* c
             S.ent_r[s] = S.perm[hi];
             S.ent_c[s] = S.perm[lo];
             S.ent_lpos[s] = ((uint32_t)lr << 16) | (uint32_t)lc;
-            if (!S.identity_dups) S.dup_ptr[s + 1] = udp[u + 1] - udp[u];
+            if (!S.identity_dups) S.dup_ptr[s + 1] = P.udp[u + 1] - P.udp[u];
         }
         if (S.identity_dups) {
-            for (int64_t u = 0; u < nu; ++u) S.dup_pos[slot_of[u]] = pr[udp[u]].second;
+            for (int64_t u = 0; u < nu; ++u) S.dup_pos[slot_of[u]] = P.pos_sorted[P.udp[u]];
         } else {
             for (int64_t s = 0; s < nu; ++s) S.dup_ptr[s + 1] += S.dup_ptr[s];
             for (int64_t u = 0; u < nu; ++u) {
                 int64_t o = S.dup_ptr[slot_of[u]];
-                for (int32_t q = udp[u]; q < udp[u + 1]; ++q) S.dup_pos[o++] = pr[q].second;  // ascending COO position
+                for (int32_t q = P.udp[u]; q < P.udp[u + 1]; ++q) S.dup_pos[o++] = P.pos_sorted[q];
             }
         }
     }
@@ -414,6 +430,40 @@ std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* c
                              [&](int32_t a, int32_t b) { return S.f_m[a] > S.f_m[b]; });
     }
     return "";
+}
+
+int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge) {
+    const int32_t nf = (int32_t)S.nf;
+    // final target of every front: follow merged fronts up to the first kept ancestor
+    std::vector<int32_t> target(nf);
+    int64_t merged = 0;
+    for (int32_t b = nf - 1; b >= 0; --b) {  // parents have larger ids
+        if (merge[b] && S.f_parent[b] >= 0) {
+            target[b] = target[S.f_parent[b]];
+            merged++;
+        } else {
+            target[b] = b;
+        }
+    }
+    if (!merged) return 0;
+    std::vector<std::vector<int32_t>> pending(nf);
+    std::vector<int32_t> perm, bfirst;
+    perm.reserve(P.n);
+    for (int32_t b = 0; b < nf; ++b) {
+        if (target[b] != b) {
+            auto& q = pending[target[b]];
+            for (int32_t j = P.bfirst[b]; j < P.bfirst[b + 1]; ++j) q.push_back(P.perm[j]);
+            continue;
+        }
+        bfirst.push_back((int32_t)perm.size());
+        perm.insert(perm.end(), pending[b].begin(), pending[b].end());  // delayed columns first
+        for (int32_t j = P.bfirst[b]; j < P.bfirst[b + 1]; ++j) perm.push_back(P.perm[j]);
+        std::vector<int32_t>().swap(pending[b]);
+    }
+    bfirst.push_back((int32_t)perm.size());
+    P.perm.swap(perm);
+    P.bfirst.swap(bfirst);
+    return merged;
 }
 
 }  // namespace ukkt

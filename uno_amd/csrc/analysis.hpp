@@ -21,6 +21,20 @@ struct AnalysisOptions {
     double dense_factor = 10.0;  // dense node: degree > max(16, dense_factor * sqrt(n))
 };
 
+// Canonical pattern + graph + ordering, kept for the lifetime of an analysis so the supernode
+// structure can be rebuilt when fronts are amalgamated after a failed pivot (delayed pivots).
+struct Pattern {
+    int64_t n = 0, nnz = 0, nu = 0;
+    std::vector<int32_t> ur, uc;            // unique entries (ur >= uc), original numbering
+    std::vector<int32_t> udp;               // nu+1: range into pos_sorted
+    std::vector<int32_t> pos_sorted;        // COO positions grouped by unique entry, ascending
+    std::vector<int64_t> ap;                // adjacency (no diagonal)
+    std::vector<int32_t> ai;
+    std::vector<int32_t> perm;              // nested-dissection order (new -> original)
+    std::vector<int32_t> bfirst;            // supernode boundaries in the new order (nb+1)
+    int64_t n_dense = 0;
+};
+
 struct Symbolic {
     int64_t n = 0, nnz = 0, nu = 0;
     // packed value slots: slot s holds unique entry (ent_r[s], ent_c[s]) in original numbering,
@@ -52,8 +66,19 @@ struct Symbolic {
     std::vector<int32_t> level_fronts; // fronts by level, each level sorted by m descending
 };
 
-// Returns "" on success, an error message otherwise.
-std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
-                    const AnalysisOptions& opt, Symbolic& out);
+// Canonicalise + order.  Returns "" on success, an error message otherwise.
+std::string order_pattern(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
+                          const AnalysisOptions& opt, Pattern& P);
+// Supernodal structure / device layout for the ordering and boundaries held in P.
+std::string build_structure(const Pattern& P, Symbolic& S);
+// Amalgamate every front flagged in `merge` into its parent (its columns are moved to just before
+// the parent's, i.e. their pivots are delayed to the parent).  Returns the number merged.
+int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge);
+
+inline std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
+                           const AnalysisOptions& opt, Pattern& P, Symbolic& S) {
+    std::string e = order_pattern(n, nnz, row, col, opt, P);
+    return e.empty() ? build_structure(P, S) : e;
+}
 
 }  // namespace ukkt

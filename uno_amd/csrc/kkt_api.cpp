@@ -61,12 +61,16 @@ struct uno_kkt {
     double u = 0.01, null_fac = 1e-5;
     int scale_iters = 1;
     int timing = 0;
+    Pattern P;
     Symbolic S;
+    int delay_relaxed = 0;      // also amalgamate fronts whose pivots needed a relaxed threshold
+    int max_merge_rounds = 64;
+    int64_t merges_total = 0;
     bool analyzed = false, factor_enqueued = false, factored = false;
     const double* values_ptr = nullptr;  // device values used by the last factorization
     // device arrays
     DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, bvec;
-    DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, child_off, child, relmap, level_fronts;
+    DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, child_off, child, relmap, level_fronts, fstat;
     DBuf<uint32_t> ent_lpos;
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off;
     DBuf<int8_t> piv;
@@ -144,11 +148,39 @@ void flush_timing(uno_kkt_t h) {
     h->pending.clear();
 }
 
+int upload_structure(uno_kkt_t h);
+int enqueue_factorization(uno_kkt_t h);
+
 int finish_factorization(uno_kkt_t h) {
     if (!h->factor_enqueued) return h->factored ? UNO_KKT_OK : set_err(h, UNO_KKT_ERR_STATE, "no factorization");
     HIPCHK(h, hipStreamSynchronize(h->stream));
     flush_timing(h);
     h->factor_enqueued = false;
+    // delayed pivots: a front that could not pivot a fully-summed column (or, optionally, needed a
+    // relaxed threshold) is amalgamated into its parent and the factorization is redone.  The merge
+    // is sticky for later factorizations of the same pattern.
+    for (int round = 0; round < h->max_merge_rounds; ++round) {
+        const unsigned long long* c = h->h_counters;
+        bool need = c[5] != 0 || (h->delay_relaxed && c[4] != 0);
+        if (!need) break;
+        std::vector<int32_t> fs(h->S.nf);
+        HIPCHK(h, hipMemcpy(fs.data(), h->fstat.p, sizeof(int32_t) * fs.size(), hipMemcpyDeviceToHost));
+        std::vector<char> merge(h->S.nf, 0);
+        for (int64_t f = 0; f < h->S.nf; ++f)
+            merge[f] = (fs[f] & 0xffff) != 0 || (h->delay_relaxed && (fs[f] >> 16) != 0);
+        int64_t merged = amalgamate(h->P, h->S, merge);
+        if (merged == 0) break;  // only roots are stuck: nothing left to merge
+        h->merges_total += merged;
+        std::string msg = build_structure(h->P, h->S);
+        if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
+        int rc = upload_structure(h);
+        if (rc != UNO_KKT_OK) return rc;
+        rc = enqueue_factorization(h);
+        if (rc != UNO_KKT_OK) return rc;
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        flush_timing(h);
+        h->factor_enqueued = false;
+    }
     const unsigned long long* c = h->h_counters;
     h->st.pivots_2x2 = (int64_t)c[3];
     h->st.pivots_null = (int64_t)c[2];
@@ -166,9 +198,137 @@ int finish_factorization(uno_kkt_t h) {
     return UNO_KKT_OK;
 }
 
+int upload_structure(uno_kkt_t h) {
+    Symbolic& S = h->S;
+    if (S.max_m > kMaxGlobalFront)
+        return set_err(h, UNO_KKT_ERR_ARG, "front of order " + std::to_string(S.max_m) + " exceeds " +
+                                               std::to_string(kMaxGlobalFront));
+    const int64_t n = S.n;
+    // global scratch for fronts too large for LDS
+    std::vector<int64_t> goff(S.nf + 1, 0);
+    int64_t gtot = 0;
+    for (int64_t f = 0; f < S.nf; ++f) {
+        goff[f] = gtot;
+        if (S.f_m[f] > kMaxLdsFront) gtot += (int64_t)S.f_m[f] * S.f_m[f];
+    }
+    hipStream_t s = h->stream;
+    HIPCHK(h, S.identity_dups ? (h->dup_ptr.release(), hipSuccess) : h->dup_ptr.upload(S.dup_ptr, s));
+    HIPCHK(h, h->dup_pos.upload(S.dup_pos, s));
+    HIPCHK(h, h->ent_r.upload(S.ent_r, s));
+    HIPCHK(h, h->ent_c.upload(S.ent_c, s));
+    HIPCHK(h, h->ent_lpos.upload(S.ent_lpos, s));
+    HIPCHK(h, h->fm.upload(S.f_m, s));
+    HIPCHK(h, h->fp.upload(S.f_p, s));
+    HIPCHK(h, h->rows_off.upload(S.f_rows_off, s));
+    HIPCHK(h, h->rows.upload(S.rows, s));
+    HIPCHK(h, h->ent_off.upload(S.f_ent_off, s));
+    HIPCHK(h, h->child_off.upload(S.f_child_off, s));
+    HIPCHK(h, h->child.upload(S.child, s));
+    HIPCHK(h, h->relmap_off.upload(S.f_relmap_off, s));
+    HIPCHK(h, h->relmap.upload(S.relmap, s));
+    HIPCHK(h, h->L_off.upload(S.f_L_off, s));
+    HIPCHK(h, h->cb_off.upload(S.f_cb_off, s));
+    HIPCHK(h, h->gscratch_off.upload(goff, s));
+    HIPCHK(h, h->level_fronts.upload(S.level_fronts, s));
+    HIPCHK(h, h->fstat.alloc(S.nf));
+    if (h->uval.n != (size_t)S.nu) HIPCHK(h, h->uval.alloc(S.nu));
+    if (h->scale.n != (size_t)n) {
+        HIPCHK(h, h->scale.alloc(n));
+        HIPCHK(h, h->rowsum.alloc(n));
+        HIPCHK(h, h->rmax.alloc(n));
+        HIPCHK(h, h->w.alloc(n));
+        HIPCHK(h, h->bvec.alloc(n));
+    }
+    HIPCHK(h, h->L.alloc(S.L_size));
+    HIPCHK(h, h->cb.alloc(S.cb_size));
+    HIPCHK(h, h->cvec.alloc(S.f_relmap_off.empty() ? 0 : S.f_relmap_off.back()));
+    HIPCHK(h, h->gscratch.alloc(gtot));
+    HIPCHK(h, h->frow.alloc(S.rows.size()));
+    HIPCHK(h, h->piv.alloc(S.rows.size()));
+    if (!h->anorm.p) {
+        HIPCHK(h, h->anorm.alloc(1));
+        HIPCHK(h, h->counters.alloc(8));
+    }
+    // launch plan: per level, fronts sorted by order (descending) -> size classes
+    h->fac_launches.clear();
+    h->level_ranges.clear();
+    h->level_mmax.clear();
+    for (int l = 0; l < S.nlevels; ++l) {
+        int b = S.level_off[l], e = S.level_off[l + 1];
+        h->level_ranges.push_back({b, e - b});
+        h->level_mmax.push_back(e > b ? S.f_m[S.level_fronts[b]] : 0);
+        int q = b;
+        while (q < e) {
+            int m0 = S.f_m[S.level_fronts[q]];
+            bool global = m0 > kMaxLdsFront;
+            int cap = global ? 1 << 30 : (m0 > 64 ? kMaxLdsFront : (m0 > 32 ? 64 : 32));
+            int floor_ = global ? kMaxLdsFront : (cap == kMaxLdsFront ? 64 : (cap == 64 ? 32 : 0));
+            int r = q;
+            while (r < e && S.f_m[S.level_fronts[r]] > floor_ && S.f_m[S.level_fronts[r]] <= cap) ++r;
+            h->fac_launches.push_back({q, r - q, m0, global});
+            q = r;
+        }
+    }
+    HIPCHK(h, hipStreamSynchronize(s));
+    double an = h->st.analysis_seconds;
+    int64_t nfac = h->st.factorizations, nsol = h->st.solves;
+    memset(&h->st, 0, sizeof(h->st));
+    h->st.n = S.n;
+    h->st.nnz = S.nnz;
+    h->st.nnz_unique = S.nu;
+    h->st.nnz_L = S.nnz_L;
+    h->st.n_fronts = S.nf;
+    h->st.n_levels = S.nlevels;
+    h->st.max_front = S.max_m;
+    h->st.n_dense = S.n_dense;
+    h->st.flops = S.flops;
+    h->st.analysis_seconds = an;
+    h->st.factorizations = nfac;
+    h->st.solves = nsol;
+    h->st.bytes_L = 8.0 * (double)S.L_size;
+    h->st.bytes_cb = 8.0 * (double)S.cb_size;
+    return UNO_KKT_OK;
+}
+
+int enqueue_factorization(uno_kkt_t h) {
+    Symbolic& S = h->S;
+    hipStream_t s = h->stream;
+    HIPCHK(h, hipMemsetAsync(h->counters.p, 0, 8 * sizeof(unsigned long long), s));
+    HIPCHK(h, hipMemsetAsync(h->anorm.p, 0, sizeof(unsigned long long), s));
+    if (S.n > 0) {
+        HIPCHK(h, hipMemsetAsync(h->rmax.p, 0, S.n * sizeof(unsigned long long), s));
+        HIPCHK(h, hipMemsetAsync(h->rowsum.p, 0, S.n * sizeof(double), s));
+    }
+    {
+        TimerScope t(h, KC_PACK);
+        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->ent_r.p, h->ent_c.p, S.nu, h->uval.p,
+                              h->scale_iters > 0 ? h->rmax.p : nullptr, s));
+    }
+    {
+        TimerScope t(h, KC_SCALE);
+        HIPCHK(h, launch_scale(h->uval.p, h->ent_r.p, h->ent_c.p, S.nu, S.n, h->scale_iters, h->scale.p, h->rmax.p,
+                               h->rowsum.p, h->anorm.p, s));
+    }
+    FactorArgs A;
+    A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
+    A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
+    A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
+    A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
+    A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.piv = h->piv.p;
+    A.counters = h->counters.p; A.fstat = h->fstat.p; A.u = h->u; A.null_fac = h->null_fac;
+    for (const Launch& L : h->fac_launches) {
+        TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
+        HIPCHK(h, launch_factor(A, h->level_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+    }
+    HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    h->factor_enqueued = true;
+    return UNO_KKT_OK;
+}
+
 }  // namespace
 
 extern "C" {
+
 
 const char* uno_kkt_version(void) { return "uno-kkt-mi355x 0.1.0 (gfx950)"; }
 
@@ -211,6 +371,8 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "max_block") h->aopt.max_block = std::max(1, std::min((int)value, 1024));
     else if (n == "dense_factor") h->aopt.dense_factor = value;
     else if (n == "timing") h->timing = value != 0.0;
+    else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
+    else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;
 }
@@ -222,89 +384,17 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
     HIPCHK(h, hipStreamSynchronize(h->stream));
     h->analyzed = h->factored = h->factor_enqueued = false;
     h->values_ptr = nullptr;
+    h->merges_total = 0;
     auto t0 = std::chrono::steady_clock::now();
-    std::string msg = ukkt::analyze(n, nnz, row, col, h->aopt, h->S);
+    std::string msg = ukkt::analyze(n, nnz, row, col, h->aopt, h->P, h->S);
     if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
-    Symbolic& S = h->S;
-    if (S.max_m > kMaxGlobalFront)
-        return set_err(h, UNO_KKT_ERR_ARG, "front of order " + std::to_string(S.max_m) + " exceeds " +
-                                               std::to_string(kMaxGlobalFront));
-    // global scratch for fronts too large for LDS
-    std::vector<int64_t> goff(S.nf + 1, 0);
-    int64_t gtot = 0;
-    for (int64_t f = 0; f < S.nf; ++f) {
-        goff[f] = gtot;
-        if (S.f_m[f] > kMaxLdsFront) gtot += (int64_t)S.f_m[f] * S.f_m[f];
-    }
-    hipStream_t s = h->stream;
     HIPCHK(h, h->values.alloc(nnz));
-    HIPCHK(h, S.identity_dups ? (h->dup_ptr.release(), hipSuccess) : h->dup_ptr.upload(S.dup_ptr, s));
-    HIPCHK(h, h->dup_pos.upload(S.dup_pos, s));
-    HIPCHK(h, h->ent_r.upload(S.ent_r, s));
-    HIPCHK(h, h->ent_c.upload(S.ent_c, s));
-    HIPCHK(h, h->ent_lpos.upload(S.ent_lpos, s));
-    HIPCHK(h, h->fm.upload(S.f_m, s));
-    HIPCHK(h, h->fp.upload(S.f_p, s));
-    HIPCHK(h, h->rows_off.upload(S.f_rows_off, s));
-    HIPCHK(h, h->rows.upload(S.rows, s));
-    HIPCHK(h, h->ent_off.upload(S.f_ent_off, s));
-    HIPCHK(h, h->child_off.upload(S.f_child_off, s));
-    HIPCHK(h, h->child.upload(S.child, s));
-    HIPCHK(h, h->relmap_off.upload(S.f_relmap_off, s));
-    HIPCHK(h, h->relmap.upload(S.relmap, s));
-    HIPCHK(h, h->L_off.upload(S.f_L_off, s));
-    HIPCHK(h, h->cb_off.upload(S.f_cb_off, s));
-    HIPCHK(h, h->gscratch_off.upload(goff, s));
-    HIPCHK(h, h->level_fronts.upload(S.level_fronts, s));
-    HIPCHK(h, h->uval.alloc(S.nu));
-    HIPCHK(h, h->scale.alloc(n));
-    HIPCHK(h, h->rowsum.alloc(n));
-    HIPCHK(h, h->rmax.alloc(n));
-    HIPCHK(h, h->w.alloc(n));
-    HIPCHK(h, h->bvec.alloc(n));
-    HIPCHK(h, h->L.alloc(S.L_size));
-    HIPCHK(h, h->cb.alloc(S.cb_size));
-    HIPCHK(h, h->cvec.alloc(S.f_relmap_off.empty() ? 0 : S.f_relmap_off.back()));
-    HIPCHK(h, h->gscratch.alloc(gtot));
-    HIPCHK(h, h->frow.alloc(S.rows.size()));
-    HIPCHK(h, h->piv.alloc(S.rows.size()));
-    HIPCHK(h, h->anorm.alloc(1));
-    HIPCHK(h, h->counters.alloc(8));
-    // launch plan: per level, fronts sorted by order (descending) -> size classes
-    h->fac_launches.clear();
-    h->level_ranges.clear();
-    h->level_mmax.clear();
-    for (int l = 0; l < S.nlevels; ++l) {
-        int b = S.level_off[l], e = S.level_off[l + 1];
-        h->level_ranges.push_back({b, e - b});
-        h->level_mmax.push_back(e > b ? S.f_m[S.level_fronts[b]] : 0);
-        int q = b;
-        while (q < e) {
-            int m0 = S.f_m[S.level_fronts[q]];
-            bool global = m0 > kMaxLdsFront;
-            int cap = global ? 1 << 30 : (m0 > 64 ? kMaxLdsFront : (m0 > 32 ? 64 : 32));
-            int floor_ = global ? kMaxLdsFront : (cap == kMaxLdsFront ? 64 : (cap == 64 ? 32 : 0));
-            int r = q;
-            while (r < e && S.f_m[S.level_fronts[r]] > floor_ && S.f_m[S.level_fronts[r]] <= cap) ++r;
-            h->fac_launches.push_back({q, r - q, m0, global});
-            q = r;
-        }
-    }
-    HIPCHK(h, hipStreamSynchronize(s));
+    int rc = upload_structure(h);
+    if (rc != UNO_KKT_OK) return rc;
     auto t1 = std::chrono::steady_clock::now();
-    memset(&h->st, 0, sizeof(h->st));
-    h->st.n = S.n;
-    h->st.nnz = S.nnz;
-    h->st.nnz_unique = S.nu;
-    h->st.nnz_L = S.nnz_L;
-    h->st.n_fronts = S.nf;
-    h->st.n_levels = S.nlevels;
-    h->st.max_front = S.max_m;
-    h->st.n_dense = S.n_dense;
-    h->st.flops = S.flops;
     h->st.analysis_seconds = std::chrono::duration<double>(t1 - t0).count();
-    h->st.bytes_L = 8.0 * (double)S.L_size;
-    h->st.bytes_cb = 8.0 * (double)S.cb_size;
+    h->st.factorizations = 0;
+    h->st.solves = 0;
     h->analyzed = true;
     h->err.clear();
     return UNO_KKT_OK;
@@ -350,7 +440,6 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     if (!h->analyzed) return set_err(h, UNO_KKT_ERR_STATE, "factorize before analyze");
     HIPCHK(h, hipSetDevice(h->device));
     Symbolic& S = h->S;
-    hipStream_t s = h->stream;
     if (h->factor_enqueued) {  // previous factorization never queried: drain it first
         int rc = finish_factorization(h);
         (void)rc;
@@ -361,38 +450,12 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     } else if (values_on_device) {
         h->values_ptr = values;
     } else {
-        if (S.nnz > 0) HIPCHK(h, hipMemcpyAsync(h->values.p, values, S.nnz * sizeof(double), hipMemcpyHostToDevice, s));
+        if (S.nnz > 0)
+            HIPCHK(h, hipMemcpyAsync(h->values.p, values, S.nnz * sizeof(double), hipMemcpyHostToDevice, h->stream));
         h->values_ptr = h->values.p;
     }
-    HIPCHK(h, hipMemsetAsync(h->counters.p, 0, 8 * sizeof(unsigned long long), s));
-    HIPCHK(h, hipMemsetAsync(h->anorm.p, 0, sizeof(unsigned long long), s));
-    if (S.n > 0) {
-        HIPCHK(h, hipMemsetAsync(h->rmax.p, 0, S.n * sizeof(unsigned long long), s));
-        HIPCHK(h, hipMemsetAsync(h->rowsum.p, 0, S.n * sizeof(double), s));
-    }
-    {
-        TimerScope t(h, KC_PACK);
-        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->ent_r.p, h->ent_c.p, S.nu, h->uval.p,
-                              h->scale_iters > 0 ? h->rmax.p : nullptr, s));
-    }
-    {
-        TimerScope t(h, KC_SCALE);
-        HIPCHK(h, launch_scale(h->uval.p, h->ent_r.p, h->ent_c.p, S.nu, S.n, h->scale_iters, h->scale.p, h->rmax.p,
-                               h->rowsum.p, h->anorm.p, s));
-    }
-    FactorArgs A;
-    A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
-    A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
-    A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
-    A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
-    A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.piv = h->piv.p;
-    A.counters = h->counters.p; A.u = h->u; A.null_fac = h->null_fac;
-    for (const Launch& L : h->fac_launches) {
-        TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
-        HIPCHK(h, launch_factor(A, h->level_fronts.p + L.begin, L.count, L.mmax, L.global, s));
-    }
-    HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    h->factor_enqueued = true;
+    int rc = enqueue_factorization(h);
+    if (rc != UNO_KKT_OK) return rc;
     h->st.factorizations++;
     return UNO_KKT_OK;
 }
@@ -459,6 +522,7 @@ int uno_kkt_stats(uno_kkt_t h, uno_kkt_stats_t* out) {
     if (!h || !out) return UNO_KKT_ERR_ARG;
     if (h->factor_enqueued) finish_factorization(h);
     *out = h->st;
+    out->fronts_merged = h->merges_total;
     return UNO_KKT_OK;
 }
 

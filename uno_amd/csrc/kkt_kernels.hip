@@ -359,6 +359,7 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, con
         }
     }
     if (tid == 0) {
+        A.fstat[f] = (int32_t)((nstuck > 0xffff ? 0xffff : nstuck) | ((nrel > 0x7fff ? 0x7fff : nrel) << 16));
         atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)npos);
         atomicAdd((unsigned long long*)&A.counters[1], (unsigned long long)nneg);
         atomicAdd((unsigned long long*)&A.counters[2], (unsigned long long)nzero);

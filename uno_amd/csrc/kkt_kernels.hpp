@@ -31,6 +31,7 @@ struct FactorArgs {
     int32_t* frow;              // row ids after pivoting (same layout as rows)
     int8_t* piv;                // pivot kinds (same layout as rows)
     unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck
+    int32_t* fstat;             // per front: stuck pivots (low 16 bits) | relaxed pivots (high 16 bits)
     double u;
     double null_fac;
 };
