@@ -1,0 +1,209 @@
+"""bench.py -- KKT factor+solve throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[2], SURVEY.md 8(d) "C3"): the arrowband interior-point KKT of
+dimension N = 1e6 (nv = 750k variables, m = 250k equality constraints, nnz ~ 2.0e7 COO entries in
+Uno's ipopt-preset layout, uno_amd/csrc/arrowband.c).  A step is one numerical LDL^T factorization
++ one inertia query + one nrhs=1 solve, after an untimed symbolic analysis; values and right-hand
+side are already resident in HBM when the timed region starts.
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): every rank
+factors and solves its own independent KKT system (independent objects, no data-path collective,
+weak scaling); value = all ranks' factor+solves / max-over-ranks time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the dominant
+kernel class (HIP events on the solver's stream, second timed pass) and `cpu_baseline` from the CPU
+oracle (oracle/kkt_oracle.c, a restatement of MUMPS -- MUMPS itself is not available here).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+PEAK_HBM_GBS = 8000.0    # MI355X HBM3E spec (MI355X_MICROARCH.md)
+PEAK_FP64_TFS = 78.6     # MI355X FP64 vector/matrix spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=1_000_000, help="KKT dimension (C3 = 1e6)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-n", type=int, default=1_000_000)
+    ap.add_argument("--profile-only", action="store_true", help="skip event pass and CPU baseline")
+    return ap.parse_args()
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl" if torch.cuda.is_available() else "gloo")
+    dev = torch.device("cuda", local)
+
+    import uno_amd
+    uno_amd.load_library()
+    seed = uno_amd.SEEDS["C3"] + rank  # independent system per rank
+    n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(args.n, seed)
+    kkt = uno_amd.HipKKT(local)
+    t0 = time.perf_counter()
+    kkt.analyze(n, rows, cols)
+    t_analysis = time.perf_counter() - t0
+
+    vals_d = torch.from_numpy(vals).to(dev)
+    rhs_d = torch.from_numpy(rhs).to(dev)
+    x_d = torch.empty_like(rhs_d)
+    torch.cuda.synchronize()
+
+    def step():
+        kkt.factorize(device_ptr=vals_d.data_ptr())
+        inertia = kkt.inertia()
+        kkt.solve_device(rhs_d.data_ptr(), x_d.data_ptr())
+        return inertia
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        inertia = step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        inertia = step()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    barrier()
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    elapsed = float(tmax.item())
+
+    # parity sanity on the measured system: relative residual of the last solve
+    x = x_d.cpu().numpy()
+    res = np.abs(uno_amd.coo_symv(n, rows, cols, vals, x) - rhs).max()
+    absk = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max()
+    rel_res = float(res / (absk * np.abs(x).max() + np.abs(rhs).max()))
+    st = kkt.stats()
+
+    # second timed pass with per-kernel HIP events on the solver stream (roofline)
+    ktimes = {}
+    if not args.profile_only:
+        kkt.set_option("timing", 1)
+        kkt.reset_kernel_times()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        ktimes = kkt.kernel_times()
+        kkt.set_option("timing", 0)
+
+    if rank != 0:
+        if world > 1:
+            dist.barrier()
+            dist.destroy_process_group()
+        return
+
+    steps_total = args.steps * world
+    value = steps_total / elapsed
+    ms_per_step = 1e3 * elapsed / args.steps
+
+    # ---- roofline of the dominant kernel class ----
+    K = args.steps
+    n2 = st["pivots_2x2"]
+    bytes_solve = 8.0 * (2 * st["nnz_L"] + n + n2) + 24.0 * n      # SURVEY 8(d) B_solve, per solve
+    flops_fac = st["flops"]                                         # per factorization
+    bytes_fac = 8.0 * (st["nnz_unique"] + st["nnz_L"] + n)          # B_min per factorization
+    roof = None
+    if ktimes:
+        fac_ms = (ktimes["factor_lds"][0] + ktimes["factor_global"][0]) / K
+        sol_ms = (ktimes["solve_fwd"][0] + ktimes["solve_bwd"][0]) / K
+        others = {k: v[0] / K for k, v in ktimes.items()}
+        if fac_ms >= sol_ms:
+            ach = flops_fac / (fac_ms * 1e-3) / 1e12
+            roof = {"kernel": "factor (k_factor_lds/k_factor_global, all level launches of one factorization)",
+                    "bound": "mfma", "achieved": round(ach, 4), "peak": PEAK_FP64_TFS, "unit": "TFLOP/s",
+                    "frac": round(ach / PEAK_FP64_TFS, 5), "traffic": None,
+                    "algorithmic": f"{flops_fac:.4e} FP64 flop per factorization",
+                    "ms_per_launch_group": round(fac_ms, 4),
+                    "hbm_view_GBs": round(bytes_fac / (fac_ms * 1e-3) / 1e9, 2)}
+        else:
+            ach = bytes_solve / (sol_ms * 1e-3) / 1e9
+            roof = {"kernel": "solve (k_solve_fwd + k_solve_bwd, all levels of one solve)",
+                    "bound": "hbm", "achieved": round(ach, 2), "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                    "frac": round(ach / PEAK_HBM_GBS, 5), "traffic": None,
+                    "algorithmic": f"{bytes_solve:.4e} B per solve", "ms_per_launch_group": round(sol_ms, 4)}
+        roof["kernel_ms_per_step"] = {k: round(v, 4) for k, v in others.items()}
+        roof["solve_GBs"] = round(bytes_solve / (sol_ms * 1e-3) / 1e9, 2) if sol_ms > 0 else None
+        pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+        if os.path.exists(pmc):
+            try:
+                roof["traffic"] = json.load(open(pmc)).get("factor_bytes_per_factorization")
+            except Exception:
+                pass
+
+    # ---- CPU baseline: the oracle (MUMPS restatement) on the host, one core ----
+    cpu = None
+    if not args.no_cpu_baseline and not args.profile_only:
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        from oracle_ffi import OracleKKT
+        cn, _, _, cr, cc, cv, cb = uno_amd.arrowband(args.cpu_baseline_n, uno_amd.SEEDS["C3"])
+        o = OracleKKT()
+        o.analyze(cn, cr, cc)
+        reps, t_cpu = 0, 0.0
+        while reps < 3 and t_cpu < 20.0:
+            t1 = time.perf_counter()
+            o.factorize(cv)
+            o.inertia()
+            o.solve(cb)
+            t_cpu += time.perf_counter() - t1
+            reps += 1
+        cpu = {"value": round(reps / t_cpu, 5), "unit": "factor+solve/s", "cores": 1, "kind": "port",
+               "sample": f"oracle/kkt_oracle.c (MUMPS sym=2 restatement; MUMPS unavailable) on arrowband "
+                         f"n={cn} nnz={len(cv)}, {reps} factor+inertia+solve reps, {t_cpu:.2f} s, 1 thread"}
+
+    out = {
+        "metric": "KKT factor+solve/sec & HBM GB/s, n=1e6 nnz=2e7 ipopt preset, 1/2/4/8 GPU",
+        "value": round(value, 4),
+        "unit": "factor+solve/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (arrowband KKT generator, SURVEY 8(d), seed 0x5EED0003+rank)",
+        "config": {"workload": "C3 arrowband KKT, ipopt-preset COO layout, factor+inertia+solve",
+                   "n": n, "nv": nv, "m": m, "nnz": int(len(vals)), "nnz_unique": st["nnz_unique"],
+                   "nnz_L": st["nnz_L"], "fronts": st["n_fronts"], "levels": st["n_levels"],
+                   "max_front": st["max_front"], "ordering": "nested dissection (BFS level sets), 6 dense nodes last",
+                   "analysis_s": round(t_analysis, 3), "inertia": list(inertia),
+                   "pivots_2x2": st["pivots_2x2"], "pivots_relaxed": st["pivots_relaxed"],
+                   "fronts_merged": st["fronts_merged"], "rel_residual": rel_res,
+                   "parallelism": f"replicas x{world} (independent KKT per GPU)"},
+        "roofline": roof,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(out))
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

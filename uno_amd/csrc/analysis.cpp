@@ -388,9 +388,47 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
     S.dup_ptr.assign(S.identity_dups ? 0 : nu + 1, 0);
     S.dup_pos.resize(nnz);
     {
-        std::vector<int64_t> fill(S.f_ent_off.begin(), S.f_ent_off.end() - 1);
+        // slots ordered by (column, row) in the new numbering: fronts are contiguous column ranges,
+        // so this is front-major and column i of the permuted lower triangle is contiguous
+        std::vector<int64_t> ccount(n + 1, 0);
+        for (int64_t u = 0; u < nu; ++u) ccount[std::min(S.iperm[P.ur[u]], S.iperm[P.uc[u]]) + 1]++;
+        for (int64_t i = 0; i < n; ++i) ccount[i + 1] += ccount[i];
+        S.cptr.assign(ccount.begin(), ccount.end());
         std::vector<int32_t> slot_of(nu);
-        for (int64_t u = 0; u < nu; ++u) slot_of[u] = (int32_t)fill[ublk[u]]++;
+        {
+            std::vector<std::pair<int32_t, int32_t>> key(nu);  // (col, row) new numbering
+            std::vector<int64_t> cf(ccount.begin(), ccount.end() - 1);
+            std::vector<int32_t> bycol(nu);
+            for (int64_t u = 0; u < nu; ++u) {
+                int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
+                bycol[cf[std::min(a, c)]++] = (int32_t)u;
+            }
+            for (int64_t i = 0; i < n; ++i) {
+                auto first = bycol.begin() + ccount[i], last = bycol.begin() + ccount[i + 1];
+                std::sort(first, last, [&](int32_t x, int32_t y) {
+                    return std::max(S.iperm[P.ur[x]], S.iperm[P.uc[x]]) < std::max(S.iperm[P.ur[y]], S.iperm[P.uc[y]]);
+                });
+            }
+            for (int64_t q = 0; q < nu; ++q) slot_of[bycol[q]] = (int32_t)q;
+        }
+        // row part: entries (i, c), c < i, listed per row i
+        S.rptr.assign(n + 1, 0);
+        for (int64_t u = 0; u < nu; ++u) {
+            int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
+            if (a != c) S.rptr[std::max(a, c) + 1]++;
+        }
+        for (int64_t i = 0; i < n; ++i) S.rptr[i + 1] += S.rptr[i];
+        S.rslot.resize(S.rptr[n]);
+        {
+            std::vector<int32_t> rf(S.rptr.begin(), S.rptr.end() - 1);
+            std::vector<int32_t> uof(nu);
+            for (int64_t u = 0; u < nu; ++u) uof[slot_of[u]] = (int32_t)u;
+            for (int64_t q = 0; q < nu; ++q) {
+                int32_t u = uof[q];
+                int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
+                if (a != c) S.rslot[rf[std::max(a, c)]++] = (int32_t)q;
+            }
+        }
         for (int64_t u = 0; u < nu; ++u) {
             int32_t s = slot_of[u], b = ublk[u];
             int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
@@ -430,6 +468,42 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
                              [&](int32_t a, int32_t b) { return S.f_m[a] > S.f_m[b]; });
     }
     return "";
+}
+
+int64_t delay_columns(Pattern& P, const Symbolic& S, const std::vector<int32_t>& delayed_vars) {
+    const int32_t nf = (int32_t)S.nf;
+    std::vector<int32_t> blk(P.n), iperm(P.n);
+    for (int32_t b = 0; b < nf; ++b)
+        for (int32_t j = P.bfirst[b]; j < P.bfirst[b + 1]; ++j) blk[j] = b;
+    for (int32_t q = 0; q < (int32_t)P.n; ++q) iperm[P.perm[q]] = q;
+    std::vector<char> moved(P.n, 0);
+    std::vector<std::vector<int32_t>> into(nf);  // new indices delayed into each block
+    int64_t count = 0;
+    for (int32_t v : delayed_vars) {
+        if (v < 0 || v >= P.n) continue;
+        int32_t j = iperm[v];
+        if (moved[j]) continue;
+        int32_t par = S.f_parent[blk[j]];
+        if (par < 0) continue;  // roots cannot delay
+        moved[j] = 1;
+        into[par].push_back(j);
+        count++;
+    }
+    if (!count) return 0;
+    std::vector<int32_t> perm, bfirst;
+    perm.reserve(P.n);
+    for (int32_t b = 0; b < nf; ++b) {
+        std::sort(into[b].begin(), into[b].end());
+        size_t start = perm.size();
+        for (int32_t j : into[b]) perm.push_back(P.perm[j]);
+        for (int32_t j = P.bfirst[b]; j < P.bfirst[b + 1]; ++j)
+            if (!moved[j]) perm.push_back(P.perm[j]);
+        if (perm.size() > start) bfirst.push_back((int32_t)start);
+    }
+    bfirst.push_back((int32_t)perm.size());
+    P.perm.swap(perm);
+    P.bfirst.swap(bfirst);
+    return count;
 }
 
 int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge) {

@@ -43,6 +43,10 @@ struct Symbolic {
     std::vector<int32_t> dup_ptr, dup_pos;
     std::vector<int32_t> ent_r, ent_c; // original ids, ent_r is the later-eliminated one
     std::vector<uint32_t> ent_lpos;    // (local row << 16) | local col inside the owning front
+    // row-wise access to the packed slots (new numbering) for atomic-free equilibration:
+    // column part of row i = slots [cptr[i], cptr[i+1]) (entries (r, i), r >= i, contiguous),
+    // row part = rslot[rptr[i] .. rptr[i+1]) (entries (i, c), c < i)
+    std::vector<int32_t> cptr, rptr, rslot;
     // ordering (new index -> original index and inverse)
     std::vector<int32_t> perm, iperm;
     int64_t n_dense = 0;
@@ -74,6 +78,9 @@ std::string build_structure(const Pattern& P, Symbolic& S);
 // Amalgamate every front flagged in `merge` into its parent (its columns are moved to just before
 // the parent's, i.e. their pivots are delayed to the parent).  Returns the number merged.
 int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge);
+// Delayed pivots at column granularity: every listed column (original id) whose front has a parent
+// is moved into its parent's block (eliminated just before the parent's own columns).
+int64_t delay_columns(Pattern& P, const Symbolic& S, const std::vector<int32_t>& delayed_vars);
 
 inline std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
                            const AnalysisOptions& opt, Pattern& P, Symbolic& S) {

@@ -63,18 +63,20 @@ struct uno_kkt {
     int timing = 0;
     Pattern P;
     Symbolic S;
-    int delay_relaxed = 0;      // also amalgamate fronts whose pivots needed a relaxed threshold
+    int delay_relaxed = 1;      // also amalgamate fronts whose pivots needed a relaxed threshold (MUMPS: delay)
     int max_merge_rounds = 64;
     int64_t merges_total = 0;
     bool analyzed = false, factor_enqueued = false, factored = false;
     const double* values_ptr = nullptr;  // device values used by the last factorization
     // device arrays
-    DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, bvec;
-    DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, child_off, child, relmap, level_fronts, fstat;
+    DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, rmax, bvec;
+    DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, level_fronts, fstat;
     DBuf<uint32_t> ent_lpos;
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off;
     DBuf<int8_t> piv;
-    DBuf<unsigned long long> rmax, anorm, counters;
+    DBuf<unsigned long long> anorm, counters;
+    DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed;
+    int32_t n_long = 0;
     unsigned long long* h_counters = nullptr;
     std::vector<Launch> fac_launches;
     std::vector<std::pair<int, int>> level_ranges;  // per level: begin, count (solve)
@@ -161,16 +163,22 @@ int finish_factorization(uno_kkt_t h) {
     // is sticky for later factorizations of the same pattern.
     for (int round = 0; round < h->max_merge_rounds; ++round) {
         const unsigned long long* c = h->h_counters;
-        bool need = c[5] != 0 || (h->delay_relaxed && c[4] != 0);
+        int64_t nd = (int64_t)std::min<unsigned long long>(c[6], (unsigned long long)h->S.n);
+        bool need = c[5] != 0 || (h->delay_relaxed && nd > 0);
         if (!need) break;
-        std::vector<int32_t> fs(h->S.nf);
-        HIPCHK(h, hipMemcpy(fs.data(), h->fstat.p, sizeof(int32_t) * fs.size(), hipMemcpyDeviceToHost));
-        std::vector<char> merge(h->S.nf, 0);
-        for (int64_t f = 0; f < h->S.nf; ++f)
-            merge[f] = (fs[f] & 0xffff) != 0 || (h->delay_relaxed && (fs[f] >> 16) != 0);
-        int64_t merged = amalgamate(h->P, h->S, merge);
-        if (merged == 0) break;  // only roots are stuck: nothing left to merge
-        h->merges_total += merged;
+        std::vector<int32_t> dv(nd);
+        if (nd > 0) HIPCHK(h, hipMemcpy(dv.data(), h->delayed.p, sizeof(int32_t) * nd, hipMemcpyDeviceToHost));
+        int64_t moved = delay_columns(h->P, h->S, dv);
+        if (moved == 0) {
+            // fall back to whole-front amalgamation for stuck fronts (cannot happen at roots)
+            std::vector<int32_t> fs(h->S.nf);
+            HIPCHK(h, hipMemcpy(fs.data(), h->fstat.p, sizeof(int32_t) * fs.size(), hipMemcpyDeviceToHost));
+            std::vector<char> merge(h->S.nf, 0);
+            for (int64_t f = 0; f < h->S.nf; ++f) merge[f] = (fs[f] & 0xffff) != 0;
+            moved = amalgamate(h->P, h->S, merge);
+        }
+        if (moved == 0) break;
+        h->merges_total += moved;
         std::string msg = build_structure(h->P, h->S);
         if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
         int rc = upload_structure(h);
@@ -231,6 +239,19 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->gscratch_off.upload(goff, s));
     HIPCHK(h, h->level_fronts.upload(S.level_fronts, s));
     HIPCHK(h, h->fstat.alloc(S.nf));
+    HIPCHK(h, h->perm_d.upload(S.perm, s));
+    HIPCHK(h, h->cptr.upload(S.cptr, s));
+    HIPCHK(h, h->rptr.upload(S.rptr, s));
+    HIPCHK(h, h->rslot.upload(S.rslot, s));
+    HIPCHK(h, h->fparent.upload(S.f_parent, s));
+    {
+        std::vector<int32_t> lr;
+        for (int64_t i = 0; i < n; ++i)
+            if ((S.cptr[i + 1] - S.cptr[i]) + (S.rptr[i + 1] - S.rptr[i]) > kLongRow) lr.push_back((int32_t)i);
+        h->n_long = (int32_t)lr.size();
+        HIPCHK(h, h->long_rows.upload(lr, s));
+    }
+    if (h->delayed.n != (size_t)std::max<int64_t>(n, 1)) HIPCHK(h, h->delayed.alloc(std::max<int64_t>(n, 1)));
     if (h->uval.n != (size_t)S.nu) HIPCHK(h, h->uval.alloc(S.nu));
     if (h->scale.n != (size_t)n) {
         HIPCHK(h, h->scale.alloc(n));
@@ -244,6 +265,7 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->cvec.alloc(S.f_relmap_off.empty() ? 0 : S.f_relmap_off.back()));
     HIPCHK(h, h->gscratch.alloc(gtot));
     HIPCHK(h, h->frow.alloc(S.rows.size()));
+    HIPCHK(h, h->fpos.alloc(S.rows.size()));
     HIPCHK(h, h->piv.alloc(S.rows.size()));
     if (!h->anorm.p) {
         HIPCHK(h, h->anorm.alloc(1));
@@ -295,27 +317,26 @@ int enqueue_factorization(uno_kkt_t h) {
     hipStream_t s = h->stream;
     HIPCHK(h, hipMemsetAsync(h->counters.p, 0, 8 * sizeof(unsigned long long), s));
     HIPCHK(h, hipMemsetAsync(h->anorm.p, 0, sizeof(unsigned long long), s));
-    if (S.n > 0) {
-        HIPCHK(h, hipMemsetAsync(h->rmax.p, 0, S.n * sizeof(unsigned long long), s));
-        HIPCHK(h, hipMemsetAsync(h->rowsum.p, 0, S.n * sizeof(double), s));
-    }
     {
         TimerScope t(h, KC_PACK);
-        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->ent_r.p, h->ent_c.p, S.nu, h->uval.p,
-                              h->scale_iters > 0 ? h->rmax.p : nullptr, s));
+        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, S.nu, h->uval.p, s));
     }
     {
         TimerScope t(h, KC_SCALE);
-        HIPCHK(h, launch_scale(h->uval.p, h->ent_r.p, h->ent_c.p, S.nu, S.n, h->scale_iters, h->scale.p, h->rmax.p,
-                               h->rowsum.p, h->anorm.p, s));
+        ScanArgs SA;
+        SA.n = S.n; SA.perm = h->perm_d.p; SA.cptr = h->cptr.p; SA.rptr = h->rptr.p; SA.rslot = h->rslot.p;
+        SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p; SA.scale = h->scale.p; SA.out = nullptr;
+        SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p; SA.n_long = h->n_long;
+        HIPCHK(h, launch_scale(SA, h->scale_iters, h->rmax.p, h->rowsum.p, s));
     }
     FactorArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
     A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
     A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
-    A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.piv = h->piv.p;
+    A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.u = h->u; A.null_fac = h->null_fac;
+    A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     for (const Launch& L : h->fac_launches) {
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
         HIPCHK(h, launch_factor(A, h->level_fronts.p + L.begin, L.count, L.mmax, L.global, s));
@@ -488,7 +509,7 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         HIPCHK(h, launch_rhs_scale(b, h->scale.p, h->w.p, S.n, s));
     }
     SolveArgs A;
-    A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.piv = h->piv.p;
+    A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
     A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p;
     for (int l = 0; l < S.nlevels; ++l) {

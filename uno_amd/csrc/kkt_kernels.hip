@@ -30,70 +30,78 @@ __device__ __forceinline__ unsigned long long as_bits(double d) { return (unsign
 // ------------------------------------------------------------------------------------------------
 
 __global__ void k_pack(const double* __restrict__ values, const int32_t* __restrict__ dup_ptr,
-                       const int32_t* __restrict__ dup_pos, const int32_t* __restrict__ ent_r,
-                       const int32_t* __restrict__ ent_c, int64_t nu, double* __restrict__ uval,
-                       unsigned long long* __restrict__ rmax) {
+                       const int32_t* __restrict__ dup_pos, int64_t nu, double* __restrict__ uval) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
         double v;
         if (dup_ptr == nullptr) {
             v = values[dup_pos[s]];
         } else {
-            v = 0.0;
+            v = 0.0;  // duplicates summed in ascending COO position (oracle order)
             for (int32_t q = dup_ptr[s]; q < dup_ptr[s + 1]; ++q) v += values[dup_pos[q]];
         }
         uval[s] = v;
-        if (rmax) {
-            unsigned long long b = as_bits(fabs(v));
-            atomicMax(rmax + ent_r[s], b);
-            atomicMax(rmax + ent_c[s], b);
-        }
     }
 }
 
-// rmax of the currently scaled matrix (sweeps 2.. of the equilibration)
-__global__ void k_rowmax_scaled(const double* __restrict__ uval, const int32_t* __restrict__ ent_r,
-                                const int32_t* __restrict__ ent_c, const double* __restrict__ scale, int64_t nu,
-                                unsigned long long* __restrict__ rmax) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
-        int32_t r = ent_r[s], c = ent_c[s];
-        unsigned long long b = as_bits(fabs(scale[r] * uval[s] * scale[c]));
-        atomicMax(rmax + r, b);
-        atomicMax(rmax + c, b);
+// Row-wise scans of the packed matrix (new numbering), atomic-free:
+//   MODE 0: rmax_i = max_j |a_ij|               (first equilibration sweep, s = 1)
+//   MODE 1: rmax_i = max_j |s_i a_ij s_j|       (later sweeps)
+//   MODE 2: rsum_i = sum_j |s_i a_ij s_j|, and max_i rsum_i -> anorm (||A_pre||_inf)
+// LPR lanes cooperate on one row; long (dense, "arrow") rows use LPR = 256 via a row list.
+template <int LPR, int MODE>
+__device__ __forceinline__ void row_scan(int32_t i, int lane, const ScanArgs& A, double* red) {
+    const int32_t orig = A.perm[i];
+    const double si = MODE > 0 ? A.scale[orig] : 1.0;
+    double acc = 0.0;
+    for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += LPR) {
+        double w = MODE == 0 ? fabs(A.uval[q]) : fabs(si * A.uval[q] * A.scale[A.ent_r[q]]);
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    for (int32_t t = A.rptr[i] + lane; t < A.rptr[i + 1]; t += LPR) {
+        const int32_t q = A.rslot[t];
+        double w = MODE == 0 ? fabs(A.uval[q]) : fabs(si * A.uval[q] * A.scale[A.ent_c[q]]);
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    const int wl = LPR < 64 ? LPR : 64;
+    for (int off = wl / 2; off > 0; off >>= 1) {
+        double o = __shfl_xor(acc, off);
+        acc = MODE == 2 ? acc + o : fmax(acc, o);
+    }
+    if (LPR > 64) {
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0)
+            for (int w = 1; w < LPR / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
+        __syncthreads();
+    }
+    if (lane == 0) {
+        A.out[orig] = acc;
+        if (MODE == 2) atomicMax(A.anorm, as_bits(acc));
     }
 }
 
-__global__ void k_scale_update(const unsigned long long* __restrict__ rmax, double* __restrict__ scale, int64_t n,
-                               int first) {
+template <int MODE>
+__global__ void k_rowscan(ScanArgs A) {
+    const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16;
+    const int lane = threadIdx.x & 15;
+    if (g >= A.n) return;
+    const int32_t i = (int32_t)g;
+    if ((A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > kLongRow) return;  // long-row kernel
+    row_scan<16, MODE>(i, lane, A, nullptr);
+}
+
+template <int MODE>
+__global__ void k_rowscan_long(ScanArgs A) {
+    __shared__ double red[kThreads / 64];
+    row_scan<kThreads, MODE>(A.long_rows[blockIdx.x], threadIdx.x, A, red);
+}
+
+__global__ void k_scale_update(const double* __restrict__ rmax, double* __restrict__ scale, int64_t n, int first) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        double r = as_double(rmax[i]);
+        double r = rmax[i];
         double s = first ? 1.0 : scale[i];
         if (r > 0.0) s = s / sqrt(r);
         scale[i] = s;
-    }
-}
-
-__global__ void k_rowsum(const double* __restrict__ uval, const int32_t* __restrict__ ent_r,
-                         const int32_t* __restrict__ ent_c, const double* __restrict__ scale, int64_t nu,
-                         double* __restrict__ rowsum) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
-        int32_t r = ent_r[s], c = ent_c[s];
-        double w = fabs(scale[r] * uval[s] * scale[c]);
-        atomicAdd(rowsum + r, w);
-        if (r != c) atomicAdd(rowsum + c, w);
-    }
-}
-
-__global__ void k_normmax(const double* __restrict__ rowsum, int64_t n, unsigned long long* __restrict__ anorm) {
-    __shared__ double red[kThreads / 64];
-    double mx = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        mx = fmax(mx, rowsum[i]);
-    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kThreads / 64; ++w) mx = fmax(mx, red[w]);
-        atomicMax(anorm, as_bits(mx));
     }
 }
 
@@ -169,13 +177,14 @@ __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int
 }
 
 // symmetric interchange of positions a < b (lower-triangle storage), all threads
-__device__ void sym_swap(double* F, int ld, int m, int a, int b, int32_t* lrow) {
+__device__ void sym_swap(double* F, int ld, int m, int a, int b, int32_t* lrow, int32_t* lorig) {
     for (int t = threadIdx.x; t < m; t += blockDim.x) {
         if (t < a) {
             double x = F[a * ld + t]; F[a * ld + t] = F[b * ld + t]; F[b * ld + t] = x;
         } else if (t == a) {
             double x = F[a * ld + a]; F[a * ld + a] = F[b * ld + b]; F[b * ld + b] = x;
             int32_t y = lrow[a]; lrow[a] = lrow[b]; lrow[b] = y;
+            y = lorig[a]; lorig[a] = lorig[b]; lorig[b] = y;
         } else if (t < b) {
             double x = F[t * ld + a]; F[t * ld + a] = F[b * ld + t]; F[b * ld + t] = x;
         } else if (t > b) {
@@ -253,12 +262,15 @@ struct FrontShared {
 // Factor one front whose lower triangle is in F (ld), fully-summed columns 0..p-1.
 // Writes L (packed trapezoid), pivot kinds, permuted row ids, CB, inertia counters.
 template <int MR>
-__device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, const FactorArgs& A, int f,
-                             FrontShared* sh) {
+__device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
+                             const FactorArgs& A, int f, FrontShared* sh) {
     const int tid = threadIdx.x;
+    for (int i = tid; i < m; i += kThreads) lorig[i] = i;  // local position before pivoting
+    __syncthreads();
     const double thres = DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits);
-    int8_t* piv = A.piv + A.rows_off[f];
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
+    bool delays_recorded = false;
+    auto lorig_var = [&](int q) { return lrow[q]; };
     int k = 0;
     while (k < p) {
         if (tid < 64) {
@@ -269,19 +281,26 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, con
         PivotDecision d = sh->dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
-            sym_swap(F, ld, m, k, d.c, lrow);
+            sym_swap(F, ld, m, k, d.c, lrow, lorig);
             __syncthreads();
         }
         if (d.kind == PIV_2X2_A) {
             int r = d.r == k ? d.c : d.r;
             if (r != k + 1) {
-                sym_swap(F, ld, m, k + 1, r, lrow);
+                sym_swap(F, ld, m, k + 1, r, lrow, lorig);
                 __syncthreads();
             }
         }
         if (tid == 0) {
             if (sh->dec.kind == PIV_STUCK) nstuck++;
             nrel += d.relaxed;
+            // first pivot that needed a relaxed threshold: the columns still fully summed would be
+            // delayed by MUMPS; report them (except at roots) so the host moves them to the parent
+            if (d.relaxed && !delays_recorded && A.record_delays && A.fparent[f] >= 0) {
+                delays_recorded = true;
+                unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
+                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lorig_var(q);
+            }
         }
         if (d.kind == PIV_NULL) {
             for (int i = k + 1 + tid; i < m; i += kThreads) F[i * ld + k] = 0.0;
@@ -343,8 +362,12 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, con
             L[t] = v;
         }
     }
-    // ---- permuted row ids (fully-summed part) ----
-    for (int i = tid; i < m; i += kThreads) A.frow[A.rows_off[f] + i] = lrow[i];
+    // ---- permuted row ids and pivot kinds ----
+    for (int i = tid; i < m; i += kThreads) {
+        A.frow[A.rows_off[f] + i] = lrow[i];
+        A.fpos[A.rows_off[f] + lorig[i]] = i;  // analysis-order local row -> pivoted position
+        if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
+    }
     // ---- contribution block: packed lower, column-major, order cm = m - p ----
     const int cm = m - p;
     if (cm > 0) {
@@ -421,8 +444,9 @@ __global__ __launch_bounds__(kThreads) void k_factor_lds(FactorArgs A, const int
     double* sloc = F + (int64_t)ld * m;
     int32_t* lrow = (int32_t*)(sloc + m);
     int32_t* rstage = lrow + m;
+    int8_t* pk = (int8_t*)(rstage + m);
     assemble_front(F, ld, m, p, lrow, sloc, rstage, A, f);
-    factor_front<MR>(F, ld, m, p, lrow, A, f, sh);
+    factor_front<MR>(F, ld, m, p, lrow, rstage, pk, A, f, sh);
 }
 
 __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const int32_t* __restrict__ fronts) {
@@ -435,8 +459,9 @@ __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const 
     double* sloc = smem + 4;
     int32_t* lrow = (int32_t*)(sloc + m);
     int32_t* rstage = lrow + m;
+    int8_t* pk = (int8_t*)(rstage + m);
     assemble_front(F, ld, m, p, lrow, sloc, rstage, A, f);
-    factor_front<0>(F, ld, m, p, lrow, A, f, sh);
+    factor_front<0>(F, ld, m, p, lrow, rstage, pk, A, f, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -473,7 +498,8 @@ __global__ __launch_bounds__(kThreads) void k_solve_fwd(SolveArgs A, const int32
         __syncthreads();
         const int32_t* rm = A.relmap + A.relmap_off[c];
         const double* cv = A.cvec + A.relmap_off[c];
-        for (int t = tid; t < cm; t += kThreads) y[rm[t]] += cv[t];
+        const int32_t* fpos = A.fpos + ro;  // this front's rows were permuted by pivoting
+        for (int t = tid; t < cm; t += kThreads) y[fpos[rm[t]]] += cv[t];
     }
     __syncthreads();
     const int64_t Lo = A.L_off[f];
@@ -558,46 +584,47 @@ static int grid_for(int64_t n, int block) {
     return (int)g;
 }
 
-hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* ent_r,
-                       const int32_t* ent_c, int64_t nu, double* uval, unsigned long long* rmax, hipStream_t s) {
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t nu, double* uval,
+                       hipStream_t s) {
     if (nu == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(nu, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, ent_r, ent_c, nu,
-                       uval, rmax);
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(nu, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, nu, uval);
     return hipGetLastError();
 }
 
-hipError_t launch_scale(const double* uval, const int32_t* ent_r, const int32_t* ent_c, int64_t nu, int64_t n,
-                        int iters, double* scale, unsigned long long* rmax, double* rowsum,
-                        unsigned long long* anorm, hipStream_t s) {
-    if (n == 0) return hipSuccess;
+template <int MODE>
+static void scan(const ScanArgs& A, hipStream_t s) {
+    const int64_t threads = A.n * 16;
+    hipLaunchKernelGGL(k_rowscan<MODE>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A);
+    if (A.n_long > 0) hipLaunchKernelGGL(k_rowscan_long<MODE>, dim3(A.n_long), dim3(kThreads), 0, s, A);
+}
+
+hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s) {
+    if (A.n == 0) return hipSuccess;
     for (int it = 0; it < iters; ++it) {
-        if (it > 0) {
-            hipMemsetAsync(rmax, 0, sizeof(unsigned long long) * n, s);
-            hipLaunchKernelGGL(k_rowmax_scaled, dim3(grid_for(nu, 256)), dim3(256), 0, s, uval, ent_r, ent_c, scale,
-                               nu, rmax);
-        }
-        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(n, 256)), dim3(256), 0, s, rmax, scale, n, it == 0 ? 1 : 0);
+        A.out = rmax;
+        if (it == 0) scan<0>(A, s);
+        else scan<1>(A, s);
+        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(A.n, 256)), dim3(256), 0, s, rmax, A.scale, A.n, it == 0 ? 1 : 0);
     }
     if (iters == 0) {  // no scaling: s = 1
-        hipMemsetAsync(rmax, 0, sizeof(unsigned long long) * n, s);
-        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(n, 256)), dim3(256), 0, s, rmax, scale, n, 1);
+        hipMemsetAsync(rmax, 0, sizeof(double) * A.n, s);
+        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(A.n, 256)), dim3(256), 0, s, rmax, A.scale, A.n, 1);
     }
-    if (nu > 0)
-        hipLaunchKernelGGL(k_rowsum, dim3(grid_for(nu, 256)), dim3(256), 0, s, uval, ent_r, ent_c, scale, nu, rowsum);
-    hipLaunchKernelGGL(k_normmax, dim3(grid_for(n, kThreads) > 1024 ? 1024 : grid_for(n, kThreads)), dim3(kThreads), 0,
-                       s, rowsum, n, anorm);
+    A.out = rowsum;
+    scan<2>(A, s);
     return hipGetLastError();
 }
 
 size_t factor_lds_bytes(int mmax) {
     int ld = mmax | 1;
-    return 32 + (size_t)ld * mmax * sizeof(double) + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t);
+    return 32 + (size_t)ld * mmax * sizeof(double) + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
+           (size_t)((mmax + 15) & ~15);
 }
 
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (global) {
-        size_t sh = 32 + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t);
+        size_t sh = 32 + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) + (size_t)((mmax + 15) & ~15);
         hipLaunchKernelGGL(k_factor_global, dim3(count), dim3(kThreads), sh, s, A, fronts);
     } else {
         size_t sh = factor_lds_bytes(mmax);

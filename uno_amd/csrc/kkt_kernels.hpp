@@ -29,9 +29,13 @@ struct FactorArgs {
     double* cb;
     double* gscratch;
     int32_t* frow;              // row ids after pivoting (same layout as rows)
+    int32_t* fpos;              // analysis-order local row -> position after pivoting
     int8_t* piv;                // pivot kinds (same layout as rows)
-    unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck
+    unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck, delayed
     int32_t* fstat;             // per front: stuck pivots (low 16 bits) | relaxed pivots (high 16 bits)
+    const int32_t* fparent;     // assembly-tree parent (-1 = root)
+    int32_t* delayed;           // original ids of columns that failed the threshold (counters[6] = count)
+    int record_delays;
     double u;
     double null_fac;
 };
@@ -41,6 +45,7 @@ struct SolveArgs {
     const int32_t* fp;
     const int64_t* rows_off;
     const int32_t* frow;
+    const int32_t* fpos;
     const int8_t* piv;
     const int32_t* child_off;
     const int32_t* child;
@@ -52,11 +57,27 @@ struct SolveArgs {
     double* cvec;   // per-front update vectors (layout of relmap)
 };
 
-hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* ent_r,
-                       const int32_t* ent_c, int64_t nu, double* uval, unsigned long long* rmax, hipStream_t s);
-hipError_t launch_scale(const double* uval, const int32_t* ent_r, const int32_t* ent_c, int64_t nu, int64_t n,
-                        int iters, double* scale, unsigned long long* rmax, double* rowsum,
-                        unsigned long long* anorm, hipStream_t s);
+// row-wise scans for the equilibration and ||A_pre||_inf (kkt_kernels.hip k_rowscan)
+struct ScanArgs {
+    int64_t n;
+    const int32_t* perm;     // new -> original
+    const int32_t* cptr;     // n+1 column part of each row (contiguous slots)
+    const int32_t* rptr;     // n+1 row part
+    const int32_t* rslot;
+    const int32_t* ent_r;    // slot -> original id of the later row
+    const int32_t* ent_c;    // slot -> original id of the earlier column
+    const double* uval;
+    double* scale;           // by original id
+    double* out;             // rmax or rowsum, by original id
+    unsigned long long* anorm;
+    const int32_t* long_rows;  // rows longer than kLongRow (new numbering)
+    int32_t n_long;
+};
+constexpr int kLongRow = 2048;
+
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t nu, double* uval,
+                       hipStream_t s);
+hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s);
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
