@@ -1,0 +1,17 @@
+/* uno_kkt_debug.h -- diagnostics of the MI355X KKT backend (not part of the Uno plugin boundary).
+ * With option "stamps" = 1 every factorization records, per front f, eight words
+ * out[8f + 0..3] = s_memrealtime (100 MHz) at kernel entry / after assembly / after the pivot loop /
+ * after write-out, out[8f+4] = pivot candidates examined, out[8f+5] = pivot steps. */
+#ifndef UNO_KKT_DEBUG_H
+#define UNO_KKT_DEBUG_H
+#include <stdint.h>
+#include "uno_kkt.h"
+#ifdef __cplusplus
+extern "C" {
+#endif
+int64_t uno_kkt_debug_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap, int32_t* front_order,
+                             int32_t* front_pivots, int32_t* front_level);
+#ifdef __cplusplus
+}
+#endif
+#endif

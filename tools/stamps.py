@@ -1,0 +1,30 @@
+"""Per-front phase timings of one C3 factorization (diagnostic build path, option stamps=1)."""
+import ctypes, os, sys
+import numpy as np
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import uno_amd
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000000
+N, nv, m, r, c, v, b = uno_amd.arrowband(n, uno_amd.SEEDS["C3"])
+g = uno_amd.HipKKT(0)
+g.analyze(N, r, c)
+g.factorize(v); g.inertia()
+g.set_option("stamps", 1)
+g.factorize(v); g.inertia()
+lib = g.lib
+nf = g.stats()["n_fronts"]
+out = np.zeros(8 * nf, dtype=np.uint64)
+fm = np.zeros(nf, dtype=np.int32); fp = np.zeros(nf, dtype=np.int32); fl = np.zeros(nf, dtype=np.int32)
+lib.uno_kkt_debug_stamps.restype = ctypes.c_int64
+P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
+k = lib.uno_kkt_debug_stamps(g.h, P(out), ctypes.c_int64(len(out)), P(fm), P(fp), P(fl))
+st = out.reshape(nf, 8).astype(np.int64)
+asm = (st[:, 1] - st[:, 0]) * 10e-3   # us
+loop = (st[:, 2] - st[:, 1]) * 10e-3
+wout = (st[:, 3] - st[:, 2]) * 10e-3
+cand = st[:, 4]; steps = st[:, 5]
+print("fronts", nf, "levels", fl.max() + 1)
+for lev in range(fl.max() + 1):
+    s = fl == lev
+    print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} p {fp[s].mean():5.1f} | assemble {asm[s].mean():7.2f} us "
+          f"loop {loop[s].mean():7.2f} us ({loop[s].mean()/max(1,steps[s].mean()):.3f} us/step, cand/step {cand[s].sum()/max(1,steps[s].sum()):.2f}) write {wout[s].mean():6.2f} us")

@@ -14,6 +14,7 @@
 #include <vector>
 
 #include "../../include/uno_kkt.h"
+#include "../../include/uno_kkt_debug.h"
 #include "analysis.hpp"
 #include "kkt_kernels.hpp"
 
@@ -72,15 +73,18 @@ struct uno_kkt {
     DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, rmax, bvec;
     DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, level_fronts, fstat;
     DBuf<uint32_t> ent_lpos;
-    DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off;
+    DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
+    DBuf<int32_t> ch_cm;
     DBuf<int8_t> piv;
-    DBuf<unsigned long long> anorm, counters;
+    DBuf<unsigned long long> anorm, counters, stamps;
+    int want_stamps = 0;
     DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed;
     int32_t n_long = 0;
+    int64_t max_long = 0;
     unsigned long long* h_counters = nullptr;
     std::vector<Launch> fac_launches;
     std::vector<std::pair<int, int>> level_ranges;  // per level: begin, count (solve)
-    std::vector<int> level_mmax;
+    std::vector<int> level_mmax, level_pmax;
     uno_kkt_stats_t st{};
     std::string err;
     // timing
@@ -232,6 +236,19 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->ent_off.upload(S.f_ent_off, s));
     HIPCHK(h, h->child_off.upload(S.f_child_off, s));
     HIPCHK(h, h->child.upload(S.child, s));
+    {
+        std::vector<int32_t> ccm(S.child.size());
+        std::vector<int64_t> crel(S.child.size()), ccb(S.child.size());
+        for (size_t q = 0; q < S.child.size(); ++q) {
+            int32_t c = S.child[q];
+            ccm[q] = S.f_m[c] - S.f_p[c];
+            crel[q] = S.f_relmap_off[c];
+            ccb[q] = S.f_cb_off[c];
+        }
+        HIPCHK(h, h->ch_cm.upload(ccm, s));
+        HIPCHK(h, h->ch_relmap_off.upload(crel, s));
+        HIPCHK(h, h->ch_cb_off.upload(ccb, s));
+    }
     HIPCHK(h, h->relmap_off.upload(S.f_relmap_off, s));
     HIPCHK(h, h->relmap.upload(S.relmap, s));
     HIPCHK(h, h->L_off.upload(S.f_L_off, s));
@@ -246,8 +263,11 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->fparent.upload(S.f_parent, s));
     {
         std::vector<int32_t> lr;
-        for (int64_t i = 0; i < n; ++i)
-            if ((S.cptr[i + 1] - S.cptr[i]) + (S.rptr[i + 1] - S.rptr[i]) > kLongRow) lr.push_back((int32_t)i);
+        h->max_long = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            int64_t len = (S.cptr[i + 1] - S.cptr[i]) + (S.rptr[i + 1] - S.rptr[i]);
+            if (len > kLongRow) { lr.push_back((int32_t)i); h->max_long = std::max(h->max_long, len); }
+        }
         h->n_long = (int32_t)lr.size();
         HIPCHK(h, h->long_rows.upload(lr, s));
     }
@@ -275,10 +295,14 @@ int upload_structure(uno_kkt_t h) {
     h->fac_launches.clear();
     h->level_ranges.clear();
     h->level_mmax.clear();
+    h->level_pmax.clear();
     for (int l = 0; l < S.nlevels; ++l) {
         int b = S.level_off[l], e = S.level_off[l + 1];
         h->level_ranges.push_back({b, e - b});
         h->level_mmax.push_back(e > b ? S.f_m[S.level_fronts[b]] : 0);
+        int pm = 0;
+        for (int q = b; q < e; ++q) pm = std::max(pm, S.f_p[S.level_fronts[q]]);
+        h->level_pmax.push_back(pm);
         int q = b;
         while (q < e) {
             int m0 = S.f_m[S.level_fronts[q]];
@@ -327,16 +351,24 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.n = S.n; SA.perm = h->perm_d.p; SA.cptr = h->cptr.p; SA.rptr = h->rptr.p; SA.rslot = h->rslot.p;
         SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p; SA.scale = h->scale.p; SA.out = nullptr;
         SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p; SA.n_long = h->n_long;
+        SA.max_long = h->max_long;
         HIPCHK(h, launch_scale(SA, h->scale_iters, h->rmax.p, h->rowsum.p, s));
     }
     FactorArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
     A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
+    A.ch_cm = h->ch_cm.p; A.ch_relmap_off = h->ch_relmap_off.p; A.ch_cb_off = h->ch_cb_off.p;
     A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
+    A.stamps = nullptr;
+    if (h->want_stamps) {
+        if (h->stamps.n != (size_t)(8 * S.nf)) HIPCHK(h, h->stamps.alloc(8 * S.nf));
+        HIPCHK(h, hipMemsetAsync(h->stamps.p, 0, sizeof(unsigned long long) * 8 * S.nf, s));
+        A.stamps = h->stamps.p;
+    }
     for (const Launch& L : h->fac_launches) {
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
         HIPCHK(h, launch_factor(A, h->level_fronts.p + L.begin, L.count, L.mmax, L.global, s));
@@ -393,6 +425,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "dense_factor") h->aopt.dense_factor = value;
     else if (n == "timing") h->timing = value != 0.0;
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
+    else if (n == "stamps") h->want_stamps = value != 0.0;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;
@@ -515,12 +548,12 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     for (int l = 0; l < S.nlevels; ++l) {
         TimerScope t(h, KC_SOLVE_FWD);
         HIPCHK(h, launch_solve(A, h->level_fronts.p + h->level_ranges[l].first, h->level_ranges[l].second,
-                               h->level_mmax[l], true, s));
+                               h->level_mmax[l], h->level_pmax[l], true, s));
     }
     for (int l = S.nlevels - 1; l >= 0; --l) {
         TimerScope t(h, KC_SOLVE_BWD);
         HIPCHK(h, launch_solve(A, h->level_fronts.p + h->level_ranges[l].first, h->level_ranges[l].second,
-                               h->level_mmax[l], false, s));
+                               h->level_mmax[l], h->level_pmax[l], false, s));
     }
     double* xd = on_device ? x : h->bvec.p;
     {
@@ -574,6 +607,17 @@ int uno_kkt_reset_kernel_times(uno_kkt_t h) {
 }
 
 void* uno_kkt_stream(uno_kkt_t h) { return h ? (void*)h->stream : nullptr; }
+
+// diagnostics (include/uno_kkt_debug.h): per-front phase stamps of the last factorization
+int64_t uno_kkt_debug_stamps(uno_kkt_t h, uint64_t* out, int64_t cap, int32_t* fm, int32_t* fp, int32_t* flevel) {
+    if (!h || !h->stamps.p) return -1;
+    if (h->factor_enqueued) finish_factorization(h);
+    int64_t nf = h->S.nf;
+    if (cap < 8 * nf) return -(8 * nf);
+    hipMemcpy(out, h->stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost);
+    for (int64_t f = 0; f < nf; ++f) { fm[f] = h->S.f_m[f]; fp[f] = h->S.f_p[f]; flevel[f] = h->S.f_level[f]; }
+    return nf;
+}
 
 const char* uno_kkt_last_error(uno_kkt_t h) { return h ? h->err.c_str() : "null handle"; }
 

@@ -19,6 +19,7 @@
 namespace ukkt {
 
 constexpr int kThreads = 256;
+template <int NT> constexpr int kGrid = NT == 64 ? 8 : 16;  // side of the Schur-update thread grid
 
 enum : int8_t { PIV_NULL = 0, PIV_1X1 = 1, PIV_2X2_A = 2, PIV_2X2_B = 3, PIV_STUCK = 4 };
 
@@ -74,10 +75,7 @@ __device__ __forceinline__ void row_scan(int32_t i, int lane, const ScanArgs& A,
             for (int w = 1; w < LPR / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
         __syncthreads();
     }
-    if (lane == 0) {
-        A.out[orig] = acc;
-        if (MODE == 2) atomicMax(A.anorm, as_bits(acc));
-    }
+    if (lane == 0) A.out[orig] = acc;
 }
 
 template <int MODE>
@@ -86,14 +84,60 @@ __global__ void k_rowscan(ScanArgs A) {
     const int lane = threadIdx.x & 15;
     if (g >= A.n) return;
     const int32_t i = (int32_t)g;
-    if ((A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > kLongRow) return;  // long-row kernel
+    if ((A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > kLongRow) {
+        if (lane == 0) A.out[A.perm[i]] = 0.0;  // combined by k_rowscan_long
+        return;
+    }
     row_scan<16, MODE>(i, lane, A, nullptr);
 }
 
+// Long (dense) rows: each row is cut into chunks of kLongChunk entries, one workgroup per chunk,
+// combined with one atomic per workgroup (a handful of rows, so contention is negligible).
 template <int MODE>
 __global__ void k_rowscan_long(ScanArgs A) {
     __shared__ double red[kThreads / 64];
-    row_scan<kThreads, MODE>(A.long_rows[blockIdx.x], threadIdx.x, A, red);
+    const int32_t i = A.long_rows[blockIdx.y];
+    const int32_t orig = A.perm[i];
+    const int32_t nc = A.cptr[i + 1] - A.cptr[i];
+    const int32_t nr = A.rptr[i + 1] - A.rptr[i];
+    const int64_t begin = (int64_t)blockIdx.x * kLongChunk;
+    if (begin >= nc + nr) return;
+    const int64_t end = begin + kLongChunk < nc + nr ? begin + kLongChunk : nc + nr;
+    const double si = MODE > 0 ? A.scale[orig] : 1.0;
+    double acc = 0.0;
+    for (int64_t t = begin + threadIdx.x; t < end; t += kThreads) {
+        int32_t q, partner;
+        if (t < nc) { q = A.cptr[i] + (int32_t)t; partner = A.ent_r[q]; }
+        else { q = A.rslot[A.rptr[i] + (int32_t)(t - nc)]; partner = A.ent_c[q]; }
+        double w = MODE == 0 ? fabs(A.uval[q]) : fabs(si * A.uval[q] * A.scale[partner]);
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        double o = __shfl_xor(acc, off);
+        acc = MODE == 2 ? acc + o : fmax(acc, o);
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kThreads / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
+        if (MODE == 2) atomicAdd(A.out + orig, acc);
+        else atomicMax((unsigned long long*)(A.out + orig), as_bits(acc));  // non-negative doubles
+    }
+}
+
+// ||A_pre||_inf = max_i rowsum_i: grid-stride block maxima, one atomic per workgroup
+__global__ void k_normmax(const double* __restrict__ rowsum, int64_t n, unsigned long long* __restrict__ anorm) {
+    __shared__ double red[kThreads / 64];
+    double mx = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        mx = fmax(mx, rowsum[i]);
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kThreads / 64; ++w) mx = fmax(mx, red[w]);
+        atomicMax(anorm, as_bits(mx));
+    }
 }
 
 __global__ void k_scale_update(const double* __restrict__ rmax, double* __restrict__ scale, int64_t n, int first) {
@@ -120,9 +164,38 @@ __device__ __forceinline__ double absA(const double* F, int ld, int i, int c) {
     return fabs(i >= c ? F[i * ld + c] : F[c * ld + i]);
 }
 
-// Threshold pivot search (MUMPS/Duff-Reid rule, u then relaxed); run by one full wave, result in
-// every lane.  Mirrors test_pivot() of oracle/kkt_oracle.c; with no delayed pivots the threshold is
-// relaxed instead of delaying.
+// ---- wave-wide reductions: DPP within 16-lane rows, readlane across rows (result wave-uniform) ----
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp64(unsigned long long x) {
+    unsigned lo = (unsigned)x, hi = (unsigned)(x >> 32);
+    lo = (unsigned)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xf, 0xf, false);
+    hi = (unsigned)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xf, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long readlane64(unsigned long long x, int l) {
+    unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
+    unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+// max over the 64 lanes of a wave (every lane must be active)
+__device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
+    x = umax64(x, dpp64<0xB1>(x));   // quad_perm [1,0,3,2]
+    x = umax64(x, dpp64<0x4E>(x));   // quad_perm [2,3,0,1]
+    x = umax64(x, dpp64<0x141>(x));  // row_half_mirror
+    x = umax64(x, dpp64<0x140>(x));  // row_mirror
+    return umax64(umax64(readlane64(x, 0), readlane64(x, 16)), umax64(readlane64(x, 32), readlane64(x, 48)));
+}
+// non-negative doubles compare like their bit patterns
+__device__ __forceinline__ double wave_max_abs(double v) { return as_double(wave_max_u64(as_bits(v))); }
+// argmax key: |v| with the 16 low mantissa bits replaced by (0xffff - i): ties -> smallest index
+__device__ __forceinline__ unsigned long long argmax_key(double av, int i) {
+    return (as_bits(av) & ~0xffffull) | (unsigned long long)(0xffff - i);
+}
+
+// Threshold pivot search (MUMPS/Duff-Reid rule, u then relaxed); run by one full wave, result
+// wave-uniform.  Mirrors test_pivot() of oracle/kkt_oracle.c; the relaxed ladder is only used at
+// roots or when delays are disabled (otherwise the first relaxation reports the delayed columns).
 __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int p, double u, double thres) {
     const int lane = threadIdx.x & 63;
     PivotDecision d{PIV_STUCK, k, -1, 0};
@@ -130,35 +203,33 @@ __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int
         // relaxation ladder u, u/10, u/100, 1e-6, 1e-10, 0 (no array: avoids scratch)
         const double uu = ul == 0 ? u : ul == 1 ? u * 0.1 : ul == 2 ? u * 0.01 : ul == 3 ? 1e-6 : ul == 4 ? 1e-10 : 0.0;
         for (int c = k; c < p; ++c) {
-            double g = 0.0, rv = 0.0;
-            int ri = 0x7fffffff;
+            double g = 0.0;
             for (int i = k + lane; i < m; i += 64) {
                 if (i == c) continue;
-                double v = absA(F, ld, i, c);
-                g = fmax(g, v);
-                if (i < p && v > rv) { rv = v; ri = i; }
+                g = fmax(g, absA(F, ld, i, c));
             }
-            for (int off = 32; off > 0; off >>= 1) {
-                g = fmax(g, __shfl_xor(g, off));
-                double orv = __shfl_xor(rv, off);
-                int ori = __shfl_xor(ri, off);
-                if (orv > rv || (orv == rv && ori < ri)) { rv = orv; ri = ori; }
-            }
+            g = wave_max_abs(g);
             const double acc = fabs(F[c * ld + c]);
             if (fmax(acc, g) <= thres) { d.kind = PIV_NULL; d.c = c; d.relaxed = ul > 0; return d; }
             if (acc != 0.0 && acc >= uu * g) { d.kind = PIV_1X1; d.c = c; d.relaxed = ul > 0; return d; }
-            if (rv > 0.0 && ri < p) {
-                const int r = ri;
+            // 1x1 rejected: largest off-diagonal among the fully-summed rows is the 2x2 partner
+            unsigned long long key = 0;
+            for (int i = k + lane; i < p; i += 64) {
+                if (i == c) continue;
+                const double v = absA(F, ld, i, c);
+                if (v > 0.0) key = umax64(key, argmax_key(v, i));
+            }
+            key = wave_max_u64(key);
+            if (key != 0) {
+                const int r = 0xffff - (int)(key & 0xffffull);
                 double gc = 0.0, gr = 0.0;
                 for (int i = k + lane; i < m; i += 64) {
                     if (i == c || i == r) continue;
                     gc = fmax(gc, absA(F, ld, i, c));
                     gr = fmax(gr, absA(F, ld, i, r));
                 }
-                for (int off = 32; off > 0; off >>= 1) {
-                    gc = fmax(gc, __shfl_xor(gc, off));
-                    gr = fmax(gr, __shfl_xor(gr, off));
-                }
+                gc = wave_max_abs(gc);
+                gr = wave_max_abs(gr);
                 const double a = F[c * ld + c];
                 const double b = r > c ? F[r * ld + c] : F[c * ld + r];
                 const double e = F[r * ld + r];
@@ -177,8 +248,9 @@ __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int
 }
 
 // symmetric interchange of positions a < b (lower-triangle storage), all threads
+template <int NT>
 __device__ void sym_swap(double* F, int ld, int m, int a, int b, int32_t* lrow, int32_t* lorig) {
-    for (int t = threadIdx.x; t < m; t += blockDim.x) {
+    for (int t = threadIdx.x; t < m; t += NT) {
         if (t < a) {
             double x = F[a * ld + t]; F[a * ld + t] = F[b * ld + t]; F[b * ld + t] = x;
         } else if (t == a) {
@@ -195,52 +267,65 @@ __device__ void sym_swap(double* F, int ld, int m, int a, int b, int32_t* lrow, 
 
 // Schur update of the trailing lower triangle after a 1x1 (TWO=false) or 2x2 pivot at k.
 // LDS variant: 16x16 thread grid, MR rows/cols per thread kept in registers.
-template <int MR, bool TWO>
+template <int G, int MR, bool TWO>
 __device__ __forceinline__ void schur_update_tile(double* F, int ld, int m, int k, double d0, double d1, double d2) {
-    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    const int ty = threadIdx.x / G, tx = threadIdx.x % G;
     const int r0 = k + (TWO ? 2 : 1);
+    // number of G-row blocks of the trailing triangle: wave-uniform, so the unrolled loops below
+    // branch out (s_cbranch) instead of issuing masked-off work for empty blocks
+    const int nb = (m - r0 + G - 1) / G;
     double ci0[MR], ci1[MR], lj0[MR], lj1[MR];
 #pragma unroll
     for (int a = 0; a < MR; ++a) {
-        int i = r0 + ty + 16 * a;
-        int j = r0 + tx + 16 * a;
+        if (a >= nb) break;
+        const int i = r0 + ty + G * a;
+        const int j = r0 + tx + G * a;
         ci0[a] = i < m ? F[i * ld + k] : 0.0;
         ci1[a] = (TWO && i < m) ? F[i * ld + k + 1] : 0.0;
-        double x0 = j < m ? F[j * ld + k] : 0.0;
-        double x1 = (TWO && j < m) ? F[j * ld + k + 1] : 0.0;
-        if (TWO) {  // [l0 l1] = [x0 x1] * inv([[d0 d1][d1 d2]])
-            lj0[a] = d2 * x0 - d1 * x1;  // scaled by 1/det below (d-values pre-divided by det)
+        const double x0 = j < m ? F[j * ld + k] : 0.0;
+        const double x1 = (TWO && j < m) ? F[j * ld + k + 1] : 0.0;
+        if (TWO) {  // [l0 l1] = [x0 x1] * inv([[d0 d1][d1 d2]]) with d pre-divided by det
+            lj0[a] = d2 * x0 - d1 * x1;
             lj1[a] = d0 * x1 - d1 * x0;
         } else {
             lj0[a] = x0 * d0;  // d0 = 1/pivot
             lj1[a] = 0.0;
         }
     }
+    // per row block: all reads, then FMAs, then writes (reads issue back to back)
 #pragma unroll
     for (int a = 0; a < MR; ++a) {
-        const int i = r0 + ty + 16 * a;
-        if (i >= m) break;
+        if (a >= nb) break;
+        const int i = r0 + ty + G * a;
+        double acc[MR];
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
-            const int j = r0 + tx + 16 * b;
-            if (j <= i) {
-                double upd = ci0[a] * lj0[b];
-                if (TWO) upd += ci1[a] * lj1[b];
-                F[i * ld + j] -= upd;
-            }
+            const int j = r0 + tx + G * b;
+            acc[b] = (i < m && j <= i) ? F[i * ld + j] : 0.0;
+        }
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            double upd = ci0[a] * lj0[b];
+            if (TWO) upd += ci1[a] * lj1[b];
+            acc[b] -= upd;
+        }
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            const int j = r0 + tx + G * b;
+            if (i < m && j <= i) F[i * ld + j] = acc[b];
         }
     }
 }
 
 // generic (global-memory) Schur update, any m
-template <bool TWO>
+template <int G, bool TWO>
 __device__ void schur_update_generic(double* F, int ld, int m, int k, double d0, double d1, double d2) {
-    const int ty = threadIdx.x >> 4, tx = threadIdx.x & 15;
+    const int ty = threadIdx.x / G, tx = threadIdx.x % G;
     const int r0 = k + (TWO ? 2 : 1);
-    for (int i = r0 + ty; i < m; i += 16) {
+    for (int i = r0 + ty; i < m; i += G) {
         const double a0 = F[i * ld + k];
         const double a1 = TWO ? F[i * ld + k + 1] : 0.0;
-        for (int j = r0 + tx; j <= i; j += 16) {
+        for (int j = r0 + tx; j <= i; j += G) {
             const double x0 = F[j * ld + k];
             double upd;
             if (TWO) {
@@ -261,11 +346,11 @@ struct FrontShared {
 
 // Factor one front whose lower triangle is in F (ld), fully-summed columns 0..p-1.
 // Writes L (packed trapezoid), pivot kinds, permuted row ids, CB, inertia counters.
-template <int MR>
+template <int NT, int MR>
 __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
-                             const FactorArgs& A, int f, FrontShared* sh) {
+                             double* coefA, double* coefB, const FactorArgs& A, int f, FrontShared* sh) {
     const int tid = threadIdx.x;
-    for (int i = tid; i < m; i += kThreads) lorig[i] = i;  // local position before pivoting
+    for (int i = tid; i < m; i += NT) lorig[i] = i;  // local position before pivoting
     __syncthreads();
     const double thres = DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits);
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
@@ -275,19 +360,22 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
     while (k < p) {
         if (tid < 64) {
             PivotDecision d = search_pivot(F, ld, m, k, p, A.u, thres);
-            if (tid == 0) sh->dec = d;
+            if (tid == 0) {
+                sh->dec = d;
+                if (A.stamps) { A.stamps[8 * f + 4] += (unsigned long long)(d.c - k + 1); A.stamps[8 * f + 5] += 1; }
+            }
         }
         __syncthreads();
         PivotDecision d = sh->dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
-            sym_swap(F, ld, m, k, d.c, lrow, lorig);
+            sym_swap<NT>(F, ld, m, k, d.c, lrow, lorig);
             __syncthreads();
         }
         if (d.kind == PIV_2X2_A) {
             int r = d.r == k ? d.c : d.r;
             if (r != k + 1) {
-                sym_swap(F, ld, m, k + 1, r, lrow, lorig);
+                sym_swap<NT>(F, ld, m, k + 1, r, lrow, lorig);
                 __syncthreads();
             }
         }
@@ -303,15 +391,15 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
             }
         }
         if (d.kind == PIV_NULL) {
-            for (int i = k + 1 + tid; i < m; i += kThreads) F[i * ld + k] = 0.0;
+            for (int i = k + 1 + tid; i < m; i += NT) F[i * ld + k] = 0.0;
             if (tid == 0) { piv[k] = PIV_NULL; nzero++; }
             __syncthreads();
             k += 1;
         } else if (d.kind == PIV_1X1) {
             const double dk = F[k * ld + k];
             const double dinv = 1.0 / dk;
-            if (MR > 0) schur_update_tile<(MR > 0 ? MR : 1), false>(F, ld, m, k, dinv, 0.0, 0.0);
-            else schur_update_generic<false>(F, ld, m, k, dinv, 0.0, 0.0);
+            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), false>(F, ld, m, k, dinv, 0.0, 0.0);
+            else schur_update_generic<kGrid<NT>, false>(F, ld, m, k, dinv, 0.0, 0.0);
             if (tid == 0) { piv[k] = PIV_1X1; if (dk > 0.0) npos++; else nneg++; }
             __syncthreads();
             k += 1;
@@ -319,8 +407,8 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
             const double a = F[k * ld + k], b = F[(k + 1) * ld + k], e = F[(k + 1) * ld + k + 1];
             const double det = a * e - b * b;
             const double idet = 1.0 / det;
-            if (MR > 0) schur_update_tile<(MR > 0 ? MR : 1), true>(F, ld, m, k, a * idet, b * idet, e * idet);
-            else schur_update_generic<true>(F, ld, m, k, a * idet, b * idet, e * idet);
+            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), true>(F, ld, m, k, a * idet, b * idet, e * idet);
+            else schur_update_generic<kGrid<NT>, true>(F, ld, m, k, a * idet, b * idet, e * idet);
             if (tid == 0) {
                 piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; n2++;
                 if (det < 0.0) { npos++; nneg++; }
@@ -331,39 +419,51 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
             k += 2;
         }
     }
+    if (A.stamps && tid == 0) A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
     // ---- write L: packed lower trapezoid, column j rows j..m-1 ----
+    // per-column coefficients first (one division per column, not per entry):
+    // L(i,j) = cA[j] * F[i][base] + cB[j] * F[i][base+1], base = j (1x1, 2x2 first) or j-1 (2x2 second)
+    for (int j = tid; j < p; j += NT) {
+        const int8_t kind = piv[j];
+        double ca = 0.0, cbv = 0.0;
+        if (kind == PIV_1X1) {
+            ca = 1.0 / F[j * ld + j];
+        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+            const int k0 = kind == PIV_2X2_A ? j : j - 1;
+            const double a = F[k0 * ld + k0], b = F[(k0 + 1) * ld + k0], e = F[(k0 + 1) * ld + k0 + 1];
+            const double idet = 1.0 / (a * e - b * b);
+            if (kind == PIV_2X2_A) { ca = e * idet; cbv = -b * idet; }
+            else { ca = -b * idet; cbv = a * idet; }
+        }
+        coefA[j] = ca;
+        coefB[j] = cbv;
+    }
+    __syncthreads();
     double* L = A.L + A.L_off[f];
     const int64_t total = (int64_t)p * m - (int64_t)p * (p - 1) / 2;
     {
         int j = 0;
         int64_t cs = 0;  // start of column j
-        for (int64_t t = tid; t < total; t += kThreads) {
+#pragma unroll 4
+        for (int64_t t = tid; t < total; t += NT) {
             while (t >= cs + (m - j)) { cs += m - j; ++j; }
             const int i = j + (int)(t - cs);
             const int8_t kind = piv[j];
             double v;
             if (i == j) {
                 v = kind == PIV_NULL ? 0.0 : F[j * ld + j];
-            } else if (kind == PIV_1X1) {
-                v = F[i * ld + j] / F[j * ld + j];
-            } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
-                const int k0 = kind == PIV_2X2_A ? j : j - 1;
-                if (kind == PIV_2X2_A && i == j + 1) {
-                    v = F[(j + 1) * ld + j];  // D off-diagonal
-                } else {
-                    const double a = F[k0 * ld + k0], b = F[(k0 + 1) * ld + k0], e = F[(k0 + 1) * ld + k0 + 1];
-                    const double det = a * e - b * b;
-                    const double x0 = F[i * ld + k0], x1 = F[i * ld + k0 + 1];
-                    v = kind == PIV_2X2_A ? (e * x0 - b * x1) / det : (a * x1 - b * x0) / det;
-                }
+            } else if (kind == PIV_2X2_A && i == j + 1) {
+                v = F[(j + 1) * ld + j];  // D off-diagonal
             } else {
-                v = 0.0;
+                const int base = kind == PIV_2X2_B ? j - 1 : j;
+                v = coefA[j] * F[i * ld + base];
+                if (kind >= PIV_2X2_A) v += coefB[j] * F[i * ld + base + 1];
             }
             L[t] = v;
         }
     }
     // ---- permuted row ids and pivot kinds ----
-    for (int i = tid; i < m; i += kThreads) {
+    for (int i = tid; i < m; i += NT) {
         A.frow[A.rows_off[f] + i] = lrow[i];
         A.fpos[A.rows_off[f] + lorig[i]] = i;  // analysis-order local row -> pivoted position
         if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
@@ -375,7 +475,8 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
         const int64_t ctot = (int64_t)cm * (cm + 1) / 2;
         int j = 0;
         int64_t cs = 0;
-        for (int64_t t = tid; t < ctot; t += kThreads) {
+#pragma unroll 4
+        for (int64_t t = tid; t < ctot; t += NT) {
             while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
             const int i = j + (int)(t - cs);
             cb[t] = F[(p + i) * ld + (p + j)];
@@ -393,48 +494,69 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
 }
 
 // assemble original entries and children contribution blocks into F (zeroed lower triangle)
+template <int NT>
 __device__ void assemble_front(double* F, int ld, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
                                const FactorArgs& A, int f) {
     const int tid = threadIdx.x;
     const int64_t ro = A.rows_off[f];
-    for (int i = tid; i < m; i += kThreads) {
+    for (int i = tid; i < m; i += NT) {
         const int32_t v = A.rows[ro + i];
         lrow[i] = v;
         sloc[i] = A.scale[v];
     }
-    for (int i = tid; i < m; i += kThreads) {
+    for (int i = tid; i < m; i += NT) {
         double* Fi = F + (int64_t)i * ld;
         for (int j = 0; j <= i; ++j) Fi[j] = 0.0;
     }
     __syncthreads();
-    for (int64_t e = A.ent_off[f] + tid; e < A.ent_off[f + 1]; e += kThreads) {
+    for (int64_t e = A.ent_off[f] + tid; e < A.ent_off[f + 1]; e += NT) {
         const uint32_t lp = A.ent_lpos[e];
         const int lr = (int)(lp >> 16), lc = (int)(lp & 0xffffu);
         F[lr * ld + lc] = sloc[lr] * A.uval[e] * sloc[lc];
     }
     for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
-        const int c = A.child[ci];
-        const int cm = A.fm[c] - A.fp[c];
+        const int cm = A.ch_cm[ci];  // child metadata stored with the edge: one load, no chain
         if (cm <= 0) continue;
         __syncthreads();  // previous child's adds done, rstage free
-        const int32_t* rm = A.relmap + A.relmap_off[c];
-        for (int i = tid; i < cm; i += kThreads) rstage[i] = rm[i];
+        const int32_t* rm = A.relmap + A.ch_relmap_off[ci];
+        for (int i = tid; i < cm; i += NT) rstage[i] = rm[i];
         __syncthreads();
-        const double* cb = A.cb + A.cb_off[c];
+        const double* cb = A.cb + A.ch_cb_off[ci];
         const int64_t ctot = (int64_t)cm * (cm + 1) / 2;
         int j = 0;
         int64_t cs = 0;
-        for (int64_t t = tid; t < ctot; t += kThreads) {
-            while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
-            const int i = j + (int)(t - cs);
-            F[rstage[i] * ld + rstage[j]] += cb[t];
+        constexpr int B = 8;  // batch: issue B global loads before the dependent LDS updates
+        for (int64_t t0 = tid; t0 < ctot; t0 += (int64_t)NT * B) {
+            double v[B];
+            int pos[B];
+#pragma unroll
+            for (int q = 0; q < B; ++q) {
+                const int64_t t = t0 + (int64_t)q * NT;
+                v[q] = t < ctot ? cb[t] : 0.0;
+            }
+#pragma unroll
+            for (int q = 0; q < B; ++q) {
+                const int64_t t = t0 + (int64_t)q * NT;
+                if (t < ctot) {
+                    while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
+                    pos[q] = rstage[j + (int)(t - cs)] * ld + rstage[j];
+                } else {
+                    pos[q] = -1;
+                }
+            }
+            double old[B];
+#pragma unroll
+            for (int q = 0; q < B; ++q) old[q] = pos[q] >= 0 ? F[pos[q]] : 0.0;
+#pragma unroll
+            for (int q = 0; q < B; ++q)
+                if (pos[q] >= 0) F[pos[q]] = old[q] + v[q];
         }
     }
     __syncthreads();
 }
 
-template <int MR>
-__global__ __launch_bounds__(kThreads) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
+template <int NT, int MR>
+__global__ __launch_bounds__(NT) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
     const int f = fronts[blockIdx.x];
@@ -442,11 +564,15 @@ __global__ __launch_bounds__(kThreads) void k_factor_lds(FactorArgs A, const int
     const int ld = m | 1;
     double* F = smem + 4;
     double* sloc = F + (int64_t)ld * m;
-    int32_t* lrow = (int32_t*)(sloc + m);
+    double* coefB = sloc + m;
+    int32_t* lrow = (int32_t*)(coefB + m);
     int32_t* rstage = lrow + m;
     int8_t* pk = (int8_t*)(rstage + m);
-    assemble_front(F, ld, m, p, lrow, sloc, rstage, A, f);
-    factor_front<MR>(F, ld, m, p, lrow, rstage, pk, A, f, sh);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
+    assemble_front<NT>(F, ld, m, p, lrow, sloc, rstage, A, f);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
+    factor_front<NT, MR>(F, ld, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
 __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const int32_t* __restrict__ fronts) {
@@ -457,11 +583,12 @@ __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const 
     const int ld = m;
     double* F = A.gscratch + A.gscratch_off[f];
     double* sloc = smem + 4;
-    int32_t* lrow = (int32_t*)(sloc + m);
+    double* coefB = sloc + m;
+    int32_t* lrow = (int32_t*)(coefB + m);
     int32_t* rstage = lrow + m;
     int8_t* pk = (int8_t*)(rstage + m);
-    assemble_front(F, ld, m, p, lrow, sloc, rstage, A, f);
-    factor_front<0>(F, ld, m, p, lrow, rstage, pk, A, f, sh);
+    assemble_front<kThreads>(F, ld, m, p, lrow, sloc, rstage, A, f);
+    factor_front<kThreads, 0>(F, ld, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -484,6 +611,27 @@ __global__ void k_unscale(const double* __restrict__ w, const double* __restrict
         x[i] = scale[i] * w[i];
 }
 
+__device__ __forceinline__ double readlane_d(double x, int l) { return as_double(readlane64(as_bits(x), l)); }
+
+// wave-wide sum (all lanes active); result wave-uniform
+__device__ __forceinline__ double wave_sum(double x) {
+    x += as_double(dpp64<0xB1>(as_bits(x)));
+    x += as_double(dpp64<0x4E>(as_bits(x)));
+    x += as_double(dpp64<0x141>(as_bits(x)));
+    x += as_double(dpp64<0x140>(as_bits(x)));
+    return (readlane_d(x, 0) + readlane_d(x, 16)) + (readlane_d(x, 32) + readlane_d(x, 48));
+}
+
+// stage the p x p lower triangle of the front's L panel into LDS (T[i*ldt + k] = L(i,k), k <= i < p)
+__device__ __forceinline__ void stage_triangle(const double* __restrict__ L, int64_t Lo, int m, int p, double* T, int ldt) {
+    for (int k = 0; k < p; ++k) {
+        const double* Lk = L + colptr(Lo, m, k);
+        for (int i = k + (int)threadIdx.x; i < p; i += kThreads) T[i * ldt + k] = Lk[i];
+    }
+}
+
+// Forward solve of one front: y <- L^{-1} y on the front rows, z = D^{-1} y on its pivots,
+// update vector of the contribution rows handed to the parent (multifrontal solve).
 __global__ __launch_bounds__(kThreads) void k_solve_fwd(SolveArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double y[];
     const int f = fronts[blockIdx.x];
@@ -491,7 +639,12 @@ __global__ __launch_bounds__(kThreads) void k_solve_fwd(SolveArgs A, const int32
     const int tid = threadIdx.x;
     const int64_t ro = A.rows_off[f];
     const int8_t* piv = A.piv + ro;
+    const int64_t Lo = A.L_off[f];
+    const bool small = p <= 64;
+    const int ldt = p | 1;
+    double* T = y + ((m + 1) & ~1);
     for (int i = tid; i < m; i += kThreads) y[i] = i < p ? A.w[A.frow[ro + i]] : 0.0;
+    if (small) stage_triangle(A.L, Lo, m, p, T, ldt);
     for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
         const int c = A.child[ci];
         const int cm = A.fm[c] - A.fp[c];
@@ -502,29 +655,54 @@ __global__ __launch_bounds__(kThreads) void k_solve_fwd(SolveArgs A, const int32
         for (int t = tid; t < cm; t += kThreads) y[fpos[rm[t]]] += cv[t];
     }
     __syncthreads();
-    const int64_t Lo = A.L_off[f];
-    for (int k = 0; k < p; ++k) {
-        const int8_t kind = piv[k];
-        if (kind == PIV_1X1) {
-            const double yk = y[k];
-            const double* Lk = A.L + colptr(Lo, m, k);
-            for (int i = k + 1 + tid; i < m; i += kThreads) y[i] -= Lk[i] * yk;
-        } else if (kind == PIV_2X2_A) {
-            const double y0 = y[k], y1 = y[k + 1];
-            const double* L0 = A.L + colptr(Lo, m, k);
-            const double* L1 = A.L + colptr(Lo, m, k + 1);
-            for (int i = k + 2 + tid; i < m; i += kThreads) y[i] -= L0[i] * y0 + L1[i] * y1;
-            ++k;
+    if (small) {
+        // triangle: one wave, lane i owns y_i, pivots broadcast by readlane (no barriers)
+        if (tid < 64) {
+            double yi = tid < p ? y[tid] : 0.0;
+            for (int k = 0; k < p; ++k) {
+                const int8_t kind = piv[k];
+                if (kind == PIV_1X1) {
+                    const double yk = readlane_d(yi, k);
+                    if (tid > k && tid < p) yi -= T[tid * ldt + k] * yk;
+                } else if (kind == PIV_2X2_A) {
+                    const double y0 = readlane_d(yi, k), y1 = readlane_d(yi, k + 1);
+                    if (tid > k + 1 && tid < p) yi -= T[tid * ldt + k] * y0 + T[tid * ldt + k + 1] * y1;
+                    ++k;
+                }
+            }
+            if (tid < p) y[tid] = yi;
         }
         __syncthreads();
+        // rectangle: contribution rows, independent dot products
+        for (int i = p + tid; i < m; i += kThreads) {
+            double acc = y[i];
+#pragma unroll 8
+            for (int k = 0; k < p; ++k) acc -= A.L[colptr(Lo, m, k) + i] * y[k];
+            y[i] = acc;
+        }
+    } else {
+        for (int k = 0; k < p; ++k) {
+            const int8_t kind = piv[k];
+            if (kind == PIV_1X1) {
+                const double yk = y[k];
+                const double* Lk = A.L + colptr(Lo, m, k);
+                for (int i = k + 1 + tid; i < m; i += kThreads) y[i] -= Lk[i] * yk;
+            } else if (kind == PIV_2X2_A) {
+                const double y0 = y[k], y1 = y[k + 1];
+                const double* L0 = A.L + colptr(Lo, m, k);
+                const double* L1 = A.L + colptr(Lo, m, k + 1);
+                for (int i = k + 2 + tid; i < m; i += kThreads) y[i] -= L0[i] * y0 + L1[i] * y1;
+                ++k;
+            }
+            __syncthreads();
+        }
     }
+    __syncthreads();
     // block diagonal
     for (int k = tid; k < p; k += kThreads) {
         const int8_t kind = piv[k];
-        double z;
         if (kind == PIV_1X1) {
-            z = y[k] / A.L[colptr(Lo, m, k) + k];
-            A.w[A.frow[ro + k]] = z;
+            A.w[A.frow[ro + k]] = y[k] / A.L[colptr(Lo, m, k) + k];
         } else if (kind == PIV_2X2_A) {
             const double a = A.L[colptr(Lo, m, k) + k], b = A.L[colptr(Lo, m, k) + k + 1];
             const double e = A.L[colptr(Lo, m, k + 1) + k + 1];
@@ -540,6 +718,7 @@ __global__ __launch_bounds__(kThreads) void k_solve_fwd(SolveArgs A, const int32
     for (int i = p + tid; i < m; i += kThreads) cv[i - p] = y[i];
 }
 
+// Backward solve of one front: x_k = z_k - sum_{i>k} L(i,k) x_i (struct rows are final, from ancestors).
 __global__ __launch_bounds__(kThreads) void k_solve_bwd(SolveArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double x[];
     const int f = fronts[blockIdx.x];
@@ -548,29 +727,46 @@ __global__ __launch_bounds__(kThreads) void k_solve_bwd(SolveArgs A, const int32
     const int64_t ro = A.rows_off[f];
     const int8_t* piv = A.piv + ro;
     const int64_t Lo = A.L_off[f];
+    const bool small = p <= 64;
+    const int ldt = p | 1;
+    double* T = x + ((m + 1) & ~1);
     for (int i = tid; i < m; i += kThreads) x[i] = A.w[A.frow[ro + i]];
+    if (small) stage_triangle(A.L, Lo, m, p, T, ldt);
     __syncthreads();
     // rectangular part: x_k -= sum_{i>=p} L(i,k) x_i, one wave per column
     for (int k = wave; k < p; k += kThreads / 64) {
         const double* Lk = A.L + colptr(Lo, m, k);
-        double s = 0.0;
-        for (int i = p + lane; i < m; i += 64) s += Lk[i] * x[i];
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        if (lane == 0 && piv[k] != PIV_NULL) x[k] -= s;
+        double sum = 0.0;
+        for (int i = p + lane; i < m; i += 64) sum += Lk[i] * x[i];
+        sum = wave_sum(sum);
+        if (lane == 0 && piv[k] != PIV_NULL) x[k] -= sum;
     }
     __syncthreads();
-    // triangle, column sweep from the last pivot
-    for (int k = p - 1; k >= 0; --k) {
-        const int8_t kind = piv[k];
-        if (kind != PIV_NULL) {
-            const double xk = x[k];
-            const int skip = kind == PIV_2X2_B ? k - 1 : -1;
-            for (int j = tid; j < k; j += kThreads)
-                if (j != skip && piv[j] != PIV_NULL) x[j] -= A.L[colptr(Lo, m, j) + k] * xk;
+    if (small) {
+        if (tid < 64) {
+            double xj = tid < p ? x[tid] : 0.0;
+            for (int k = p - 1; k >= 0; --k) {
+                const int8_t kind = piv[k];
+                if (kind == PIV_NULL) continue;
+                const double xk = readlane_d(xj, k);
+                const int skip = kind == PIV_2X2_B ? k - 1 : -1;
+                if (tid < k && tid != skip && piv[tid] != PIV_NULL) xj -= T[k * ldt + tid] * xk;
+            }
+            if (tid < p) A.w[A.frow[ro + tid]] = xj;
         }
-        __syncthreads();
+    } else {
+        for (int k = p - 1; k >= 0; --k) {
+            const int8_t kind = piv[k];
+            if (kind != PIV_NULL) {
+                const double xk = x[k];
+                const int skip = kind == PIV_2X2_B ? k - 1 : -1;
+                for (int j = tid; j < k; j += kThreads)
+                    if (j != skip && piv[j] != PIV_NULL) x[j] -= A.L[colptr(Lo, m, j) + k] * xk;
+            }
+            __syncthreads();
+        }
+        for (int k = tid; k < p; k += kThreads) A.w[A.frow[ro + k]] = x[k];
     }
-    for (int k = tid; k < p; k += kThreads) A.w[A.frow[ro + k]] = x[k];
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -595,7 +791,14 @@ template <int MODE>
 static void scan(const ScanArgs& A, hipStream_t s) {
     const int64_t threads = A.n * 16;
     hipLaunchKernelGGL(k_rowscan<MODE>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A);
-    if (A.n_long > 0) hipLaunchKernelGGL(k_rowscan_long<MODE>, dim3(A.n_long), dim3(kThreads), 0, s, A);
+    if (A.n_long > 0) {
+        hipLaunchKernelGGL(k_rowscan_long<MODE>, dim3((unsigned)((A.max_long + kLongChunk - 1) / kLongChunk), A.n_long),
+                           dim3(kThreads), 0, s, A);
+    }
+    if (MODE == 2) {
+        int g = grid_for(A.n, kThreads);
+        hipLaunchKernelGGL(k_normmax, dim3(g > 512 ? 512 : g), dim3(kThreads), 0, s, A.out, A.n, A.anorm);
+    }
 }
 
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s) {
@@ -617,20 +820,22 @@ hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hip
 
 size_t factor_lds_bytes(int mmax) {
     int ld = mmax | 1;
-    return 32 + (size_t)ld * mmax * sizeof(double) + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
+    return 32 + (size_t)ld * mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
            (size_t)((mmax + 15) & ~15);
 }
 
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (global) {
-        size_t sh = 32 + (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) + (size_t)((mmax + 15) & ~15);
+        size_t sh = 32 + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) + (size_t)((mmax + 15) & ~15);
         hipLaunchKernelGGL(k_factor_global, dim3(count), dim3(kThreads), sh, s, A, fronts);
     } else {
         size_t sh = factor_lds_bytes(mmax);
-        if (mmax <= 32) hipLaunchKernelGGL(k_factor_lds<2>, dim3(count), dim3(kThreads), sh, s, A, fronts);
-        else if (mmax <= 64) hipLaunchKernelGGL(k_factor_lds<4>, dim3(count), dim3(kThreads), sh, s, A, fronts);
-        else hipLaunchKernelGGL(k_factor_lds<8>, dim3(count), dim3(kThreads), sh, s, A, fronts);
+        // small fronts: one wave per front (no cross-wave barriers, more fronts per CU);
+        // larger fronts: four waves on a 16x16 update grid
+        if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
+        else if (mmax <= 64) hipLaunchKernelGGL((k_factor_lds<64, 8>), dim3(count), dim3(64), sh, s, A, fronts);
+        else hipLaunchKernelGGL((k_factor_lds<kThreads, 8>), dim3(count), dim3(kThreads), sh, s, A, fronts);
     }
     return hipGetLastError();
 }
@@ -647,9 +852,11 @@ hipError_t launch_unscale(const double* w, const double* scale, double* x, int64
     return hipGetLastError();
 }
 
-hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, bool forward, hipStream_t s) {
+hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
+                        hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    size_t sh = (size_t)mmax * sizeof(double) + 16;
+    size_t tri = pmax <= 64 ? (size_t)pmax * (pmax | 1) * sizeof(double) : 0;
+    size_t sh = (size_t)((mmax + 1) & ~1) * sizeof(double) + tri + 16;
     if (forward) hipLaunchKernelGGL(k_solve_fwd, dim3(count), dim3(kThreads), sh, s, A, fronts);
     else hipLaunchKernelGGL(k_solve_bwd, dim3(count), dim3(kThreads), sh, s, A, fronts);
     return hipGetLastError();

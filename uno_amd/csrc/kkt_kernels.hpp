@@ -19,6 +19,9 @@ struct FactorArgs {
     const double* scale;        // equilibration, by original id
     const int32_t* child_off;   // nf+1
     const int32_t* child;
+    const int32_t* ch_cm;       // per child edge (aligned with child): contribution-block order
+    const int64_t* ch_relmap_off;
+    const int64_t* ch_cb_off;
     const int64_t* relmap_off;  // per front: cb rows into relmap / cvec
     const int32_t* relmap;
     const int64_t* L_off;
@@ -36,6 +39,7 @@ struct FactorArgs {
     const int32_t* fparent;     // assembly-tree parent (-1 = root)
     int32_t* delayed;           // original ids of columns that failed the threshold (counters[6] = count)
     int record_delays;
+    unsigned long long* stamps;  // diagnostics (nullptr in normal runs): per front 8 words
     double u;
     double null_fac;
 };
@@ -72,8 +76,10 @@ struct ScanArgs {
     unsigned long long* anorm;
     const int32_t* long_rows;  // rows longer than kLongRow (new numbering)
     int32_t n_long;
+    int64_t max_long;          // longest row length among long_rows
 };
 constexpr int kLongRow = 2048;
+constexpr int kLongChunk = 4096;
 
 hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t nu, double* uval,
                        hipStream_t s);
@@ -82,7 +88,8 @@ size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
-hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, bool forward, hipStream_t s);
+hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
+                        hipStream_t s);
 
 constexpr int kMaxLdsFront = 128;     // fronts up to this order factor entirely in LDS
 constexpr int kMaxGlobalFront = 8192; // larger fronts are rejected at analysis
