@@ -1,0 +1,145 @@
+// HIPLDLSolver.cpp -- see HIPLDLSolver.hpp.  Each method names the MUMPS call it replaces.
+#include "HIPLDLSolver.hpp"
+
+#include <stdexcept>
+#include <string>
+
+#include "KKTTrace.hpp"
+#include "ingredients/subproblem/Subproblem.hpp"
+#include "linear_algebra/SymmetricMatrix.hpp"
+#include "optimization/WarmstartInformation.hpp"
+
+namespace uno {
+   namespace {
+      void* hip_create() {
+         uno_kkt_t h = nullptr;
+         return uno_kkt_create(&h, 0) == UNO_KKT_OK ? h : nullptr;
+      }
+      void hip_destroy(void* h) { uno_kkt_destroy(static_cast<uno_kkt_t>(h)); }
+      int hip_analyze(void* h, int64_t n, int64_t nnz, const int64_t* r, const int64_t* c) {
+         return uno_kkt_analyze(static_cast<uno_kkt_t>(h), n, nnz, r, c);
+      }
+      int hip_factorize(void* h, const double* v) { return uno_kkt_factorize(static_cast<uno_kkt_t>(h), v, 0); }
+      int hip_inertia(void* h, int64_t* p, int64_t* q, int64_t* z) {
+         return uno_kkt_inertia(static_cast<uno_kkt_t>(h), p, q, z);
+      }
+      int hip_solve(void* h, const double* b, double* x) { return uno_kkt_solve(static_cast<uno_kkt_t>(h), b, x, 0); }
+      const char* hip_last_error(void* h) { return uno_kkt_last_error(static_cast<uno_kkt_t>(h)); }
+   } // namespace
+
+   const KKTBackend& hip_kkt_backend() {
+      static const KKTBackend backend{"HIPLDL", hip_create, hip_destroy, hip_analyze, hip_factorize, hip_inertia, hip_solve,
+         hip_last_error};
+      return backend;
+   }
+
+   HIPLDLSolver::HIPLDLSolver(const KKTBackend& backend): DirectSymmetricIndefiniteLinearSolver(), backend(backend) {
+      // MUMPSSolver.cpp:16-37 (JOB=-1, ICNTL settings): pivot threshold, null-pivot detection and
+      // equilibration are the library defaults (u = 0.01, eps*1e-5*||A||, iterative scaling)
+      this->handle = this->backend.create();
+      if (this->handle == nullptr) {
+         throw std::runtime_error(std::string(this->backend.name) + ": could not create a solver (no device?)");
+      }
+   }
+
+   HIPLDLSolver::~HIPLDLSolver() {
+      this->backend.destroy(this->handle);  // MUMPSSolver.cpp:46-49 (JOB=-2)
+   }
+
+   void HIPLDLSolver::check(int status, const char* what) const {
+      if (status != 0) {
+         std::string message = std::string(this->backend.name) + " " + what + " failed (" + std::to_string(status) + "): " +
+            this->backend.last_error(this->handle);
+         throw std::runtime_error(message);
+      }
+   }
+
+   // MUMPSSolver.cpp:51-70
+   void HIPLDLSolver::initialize_memory(size_t number_variables, size_t number_constraints, size_t number_hessian_nonzeros,
+         size_t regularization_size) {
+      this->dimension = number_variables + number_constraints;
+      const size_t number_nonzeros = number_hessian_nonzeros + regularization_size;
+      this->row_indices.reserve(number_nonzeros);
+      this->column_indices.reserve(number_nonzeros);
+      this->objective_gradient.resize(number_variables);
+      this->constraints.resize(number_constraints);
+      this->constraint_jacobian.resize(number_constraints, number_variables);
+      this->augmented_matrix = SparseSymmetricMatrix<COOFormat<size_t, double>>(this->dimension, number_hessian_nonzeros,
+         regularization_size);
+      this->rhs.resize(this->dimension);
+      this->solution.resize(this->dimension);
+   }
+
+   // MUMPSSolver.cpp:72-83 + save_sparsity_to_local_format :149-157 (JOB=1)
+   void HIPLDLSolver::do_symbolic_analysis(const SymmetricMatrix<size_t, double>& matrix) {
+      this->row_indices.clear();
+      this->column_indices.clear();
+      for (const auto [row_index, column_index, _]: matrix) {
+         this->row_indices.emplace_back(static_cast<int64_t>(row_index));
+         this->column_indices.emplace_back(static_cast<int64_t>(column_index));
+      }
+      this->dimension = matrix.dimension();
+      this->analysed_nonzeros = matrix.number_nonzeros();
+      this->check(this->backend.analyze(this->handle, static_cast<int64_t>(matrix.dimension()),
+         static_cast<int64_t>(this->row_indices.size()), this->row_indices.data(), this->column_indices.data()), "analyze");
+   }
+
+   // MUMPSSolver.cpp:85-89 (JOB=2): values straight from the COO storage, no copy on the host
+   void HIPLDLSolver::do_numerical_factorization(const SymmetricMatrix<size_t, double>& matrix) {
+      if (matrix.number_nonzeros() != this->analysed_nonzeros) {
+         throw std::runtime_error("HIPLDL: the pattern changed since the symbolic analysis");
+      }
+      this->check(this->backend.factorize(this->handle, matrix.data_pointer()), "factorize");
+      this->check(this->backend.inertia(this->handle, &this->positive, &this->negative, &this->zero), "inertia");
+      kkt_trace::record_factorization(this->dimension, this->positive, this->negative, this->zero);
+   }
+
+   // MUMPSSolver.cpp:91-96 (JOB=3): the matrix argument is ignored, the last factorization is used
+   void HIPLDLSolver::solve_indefinite_system(const SymmetricMatrix<size_t, double>& /*matrix*/, const Vector<double>& rhs,
+         Vector<double>& result) {
+      this->check(this->backend.solve(this->handle, rhs.data(), result.data()), "solve");
+      kkt_trace::record_solve(this->dimension);
+   }
+
+   // MUMPSSolver.cpp:98-122: evaluate, assemble, regularize (analysis + factorizations), rhs, solve,
+   // primal-dual direction -- the orchestration every Uno plugin repeats
+   void HIPLDLSolver::solve_indefinite_system(Statistics& statistics, const Subproblem& subproblem, Direction& direction,
+         const WarmstartInformation& warmstart_information) {
+      if (warmstart_information.objective_changed) {
+         subproblem.evaluate_objective_gradient(this->objective_gradient);
+      }
+      if (warmstart_information.constraints_changed) {
+         subproblem.evaluate_constraints(this->constraints);
+         subproblem.evaluate_jacobian(this->constraint_jacobian);
+      }
+      if (warmstart_information.objective_changed || warmstart_information.constraints_changed) {
+         this->augmented_matrix.reset();
+         subproblem.assemble_augmented_matrix(statistics, this->augmented_matrix, this->constraint_jacobian);
+         subproblem.regularize_augmented_matrix(statistics, this->augmented_matrix, subproblem.dual_regularization_factor(), *this);
+         subproblem.assemble_augmented_rhs(this->objective_gradient, this->constraints, this->constraint_jacobian, this->rhs);
+      }
+      this->solve_indefinite_system(this->augmented_matrix, this->rhs, this->solution);
+      subproblem.assemble_primal_dual_direction(this->solution, direction);
+   }
+
+   // MUMPSSolver.cpp:124-147 (INFOG(12), INFOG(28))
+   Inertia HIPLDLSolver::get_inertia() const {
+      return {static_cast<size_t>(this->positive), static_cast<size_t>(this->negative), static_cast<size_t>(this->zero)};
+   }
+
+   size_t HIPLDLSolver::number_negative_eigenvalues() const {
+      return static_cast<size_t>(this->negative);
+   }
+
+   size_t HIPLDLSolver::number_zero_eigenvalues() const {
+      return static_cast<size_t>(this->zero);
+   }
+
+   bool HIPLDLSolver::matrix_is_singular() const {
+      return this->zero > 0;
+   }
+
+   size_t HIPLDLSolver::rank() const {
+      return this->dimension - static_cast<size_t>(this->zero);
+   }
+} // namespace

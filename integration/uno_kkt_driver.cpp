@@ -1,0 +1,87 @@
+// uno_kkt_driver.cpp -- runs the reference Uno core (libuno built from /root/reference by
+// oracle/ref/Makefile) on a hand-coded model with a KKT plugin chosen by linear_solver=..., and prints
+// one JSON object: status, iterations, solution and the sequence of (dimension, inertia) of every
+// factorization the plugin performed.  This is the in-container stand-in for `uno_ampl model.nl -AMPL
+// preset=ipopt linear_solver=HIPLDL` (bindings/AMPL/uno_ampl.cpp:78-139; ASL is not available).
+//
+// usage: uno_kkt_driver <model> [option=value ...]     model: hs015
+#include <cstdio>
+#include <iostream>
+#include <memory>
+#include <string>
+
+#include "KKTTrace.hpp"
+#include "Uno.hpp"
+#include "model/ModelFactory.hpp"
+#include "models/HS015Model.hpp"
+#include "optimization/Iterate.hpp"
+#include "optimization/Result.hpp"
+#include "options/DefaultOptions.hpp"
+#include "options/Options.hpp"
+#include "options/Presets.hpp"
+#include "tools/Logger.hpp"
+#include "tools/UserCallbacks.hpp"
+
+using namespace uno;
+
+int main(int argc, char* argv[]) {
+   if (argc < 2) {
+      std::cerr << "usage: " << argv[0] << " hs015 [option=value ...]\n";
+      return 2;
+   }
+   const std::string model_name = argv[1];
+   try {
+      // option precedence of uno_ampl.cpp:106-128: defaults -> solvers -> preset -> command line
+      Options options = DefaultOptions::load();
+      options.overwrite_with(DefaultOptions::determine_solvers());
+      Options command_line = Options::get_command_line_options(argc, argv, 2);
+      const auto preset = command_line.get_string_optional("preset");
+      options.overwrite_with(Presets::get_preset_options(preset.has_value() ? preset : std::optional<std::string>("ipopt")));
+      options.overwrite_with(command_line);
+      Logger::set_logger(options.get_string("logger"));
+
+      std::unique_ptr<Model> model;
+      if (model_name == "hs015") {
+         model = std::make_unique<HS015Model>();
+      }
+      else {
+         throw std::invalid_argument("unknown model " + model_name);
+      }
+      model = ModelFactory::reformulate(std::move(model), options);
+      Iterate initial_iterate(model->number_variables, model->number_constraints);
+      model->initial_primal_point(initial_iterate.primals);
+      model->project_onto_variable_bounds(initial_iterate.primals);
+      model->initial_dual_point(initial_iterate.multipliers.constraints);
+      initial_iterate.feasibility_multipliers.reset();
+
+      Uno uno{model->number_constraints, options};
+      NoUserCallbacks callbacks{};
+      const Result result = uno.solve(*model, initial_iterate, options, callbacks);
+
+      std::printf("{\"model\": \"%s\", \"linear_solver\": \"%s\", \"status\": %d, \"iterations\": %zu, \"objective\": %.17g",
+         model_name.c_str(), options.get_string("linear_solver").c_str(), static_cast<int>(result.optimization_status),
+         result.iteration, result.solution.evaluations.objective);
+      std::printf(", \"primals\": [");
+      for (size_t i = 0; i < result.number_variables; ++i) {
+         std::printf("%s%.17g", i ? ", " : "", result.solution.primals[i]);
+      }
+      size_t nf = 0, ns = 0;
+      for (const auto& e: kkt_trace::events()) {
+         (e.kind == 'F' ? nf : ns)++;
+      }
+      std::printf("], \"factorizations\": %zu, \"solves\": %zu, \"inertia_trace\": [", nf, ns);
+      bool first = true;
+      for (const auto& e: kkt_trace::events()) {
+         if (e.kind != 'F') continue;
+         std::printf("%s[%zu, %lld, %lld, %lld]", first ? "" : ", ", e.dimension, static_cast<long long>(e.positive),
+            static_cast<long long>(e.negative), static_cast<long long>(e.zero));
+         first = false;
+      }
+      std::printf("]}\n");
+   }
+   catch (std::exception& exception) {
+      std::printf("{\"error\": \"%s\"}\n", exception.what());
+      return 1;
+   }
+   return 0;
+}
