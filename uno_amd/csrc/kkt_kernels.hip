@@ -152,6 +152,20 @@ __global__ void k_scale_update(const double* __restrict__ rmax, double* __restri
 // ------------------------------------------------------------------------------------------------
 // dense front factorization
 // ------------------------------------------------------------------------------------------------
+// Front storage: only the lower triangle A(i,j), j <= i, is kept.
+//   PackedStore: row-packed lower triangle in LDS, m(m+1)/2 doubles (row i starts at i(i+1)/2)
+//   FullStore:   m x ld square (fronts too large for LDS live in HBM scratch)
+struct PackedStore {
+    double* F;
+    __device__ __forceinline__ int idx(int i, int j) const { return ((i * (i + 1)) >> 1) + j; }
+    __device__ __forceinline__ double& at(int i, int j) const { return F[idx(i, j)]; }
+};
+struct FullStore {
+    double* F;
+    int ld;
+    __device__ __forceinline__ int idx(int i, int j) const { return i * ld + j; }
+    __device__ __forceinline__ double& at(int i, int j) const { return F[idx(i, j)]; }
+};
 
 struct PivotDecision {
     int kind;  // PIV_*
@@ -159,9 +173,10 @@ struct PivotDecision {
     int relaxed;
 };
 
-// |A(i,c)| with lower-triangle storage
-__device__ __forceinline__ double absA(const double* F, int ld, int i, int c) {
-    return fabs(i >= c ? F[i * ld + c] : F[c * ld + i]);
+// |A(i,c)| of the symmetric front from its lower triangle
+template <class S>
+__device__ __forceinline__ double absA(const S& st, int i, int c) {
+    return fabs(i >= c ? st.at(i, c) : st.at(c, i));
 }
 
 // ---- wave-wide reductions: DPP within 16-lane rows, readlane across rows (result wave-uniform) ----
@@ -196,7 +211,8 @@ __device__ __forceinline__ unsigned long long argmax_key(double av, int i) {
 // Threshold pivot search (MUMPS/Duff-Reid rule, u then relaxed); run by one full wave, result
 // wave-uniform.  Mirrors test_pivot() of oracle/kkt_oracle.c; the relaxed ladder is only used at
 // roots or when delays are disabled (otherwise the first relaxation reports the delayed columns).
-__device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int p, double u, double thres) {
+template <class S>
+__device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u, double thres) {
     const int lane = threadIdx.x & 63;
     PivotDecision d{PIV_STUCK, k, -1, 0};
     for (int ul = 0; ul < 6; ++ul) {
@@ -206,17 +222,17 @@ __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int
             double g = 0.0;
             for (int i = k + lane; i < m; i += 64) {
                 if (i == c) continue;
-                g = fmax(g, absA(F, ld, i, c));
+                g = fmax(g, absA(st, i, c));
             }
             g = wave_max_abs(g);
-            const double acc = fabs(F[c * ld + c]);
+            const double acc = fabs(st.at(c, c));
             if (fmax(acc, g) <= thres) { d.kind = PIV_NULL; d.c = c; d.relaxed = ul > 0; return d; }
             if (acc != 0.0 && acc >= uu * g) { d.kind = PIV_1X1; d.c = c; d.relaxed = ul > 0; return d; }
             // 1x1 rejected: largest off-diagonal among the fully-summed rows is the 2x2 partner
             unsigned long long key = 0;
             for (int i = k + lane; i < p; i += 64) {
                 if (i == c) continue;
-                const double v = absA(F, ld, i, c);
+                const double v = absA(st, i, c);
                 if (v > 0.0) key = umax64(key, argmax_key(v, i));
             }
             key = wave_max_u64(key);
@@ -225,14 +241,14 @@ __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int
                 double gc = 0.0, gr = 0.0;
                 for (int i = k + lane; i < m; i += 64) {
                     if (i == c || i == r) continue;
-                    gc = fmax(gc, absA(F, ld, i, c));
-                    gr = fmax(gr, absA(F, ld, i, r));
+                    gc = fmax(gc, absA(st, i, c));
+                    gr = fmax(gr, absA(st, i, r));
                 }
                 gc = wave_max_abs(gc);
                 gr = wave_max_abs(gr);
-                const double a = F[c * ld + c];
-                const double b = r > c ? F[r * ld + c] : F[c * ld + r];
-                const double e = F[r * ld + r];
+                const double a = st.at(c, c);
+                const double b = r > c ? st.at(r, c) : st.at(c, r);
+                const double e = st.at(r, r);
                 const double det = a * e - b * b;
                 if (det != 0.0) {
                     const double lim = uu > 0.0 ? fabs(det) / uu : INFINITY;
@@ -247,28 +263,40 @@ __device__ PivotDecision search_pivot(const double* F, int ld, int m, int k, int
     return d;
 }
 
+// Fast path of the same rule for the first candidate (c = k): every lane tests its own entries
+// u*|a_ik| <= |a_kk| and one ballot decides; equivalent to search_pivot's first 1x1 acceptance
+// (|a_kk| > thres excludes the null case, so fmax(|a_kk|, g) > thres).  Run by one full wave.
+template <class S>
+__device__ __forceinline__ bool quick_1x1(const S& st, int m, int k, double u, double thres) {
+    const int lane = threadIdx.x & 63;
+    const double akk = fabs(st.at(k, k));
+    bool bad = !(akk > thres);
+    for (int i = k + 1 + lane; i < m; i += 64) bad |= u * fabs(st.at(i, k)) > akk;
+    return __ballot(bad) == 0;
+}
+
 // symmetric interchange of positions a < b (lower-triangle storage), all threads
-template <int NT>
-__device__ void sym_swap(double* F, int ld, int m, int a, int b, int32_t* lrow, int32_t* lorig) {
+template <int NT, class S>
+__device__ void sym_swap(const S& st, int m, int a, int b, int32_t* lrow, int32_t* lorig) {
     for (int t = threadIdx.x; t < m; t += NT) {
         if (t < a) {
-            double x = F[a * ld + t]; F[a * ld + t] = F[b * ld + t]; F[b * ld + t] = x;
+            double x = st.at(a, t); st.at(a, t) = st.at(b, t); st.at(b, t) = x;
         } else if (t == a) {
-            double x = F[a * ld + a]; F[a * ld + a] = F[b * ld + b]; F[b * ld + b] = x;
+            double x = st.at(a, a); st.at(a, a) = st.at(b, b); st.at(b, b) = x;
             int32_t y = lrow[a]; lrow[a] = lrow[b]; lrow[b] = y;
             y = lorig[a]; lorig[a] = lorig[b]; lorig[b] = y;
         } else if (t < b) {
-            double x = F[t * ld + a]; F[t * ld + a] = F[b * ld + t]; F[b * ld + t] = x;
+            double x = st.at(t, a); st.at(t, a) = st.at(b, t); st.at(b, t) = x;
         } else if (t > b) {
-            double x = F[t * ld + a]; F[t * ld + a] = F[t * ld + b]; F[t * ld + b] = x;
+            double x = st.at(t, a); st.at(t, a) = st.at(t, b); st.at(t, b) = x;
         }
     }
 }
 
 // Schur update of the trailing lower triangle after a 1x1 (TWO=false) or 2x2 pivot at k.
-// LDS variant: 16x16 thread grid, MR rows/cols per thread kept in registers.
-template <int G, int MR, bool TWO>
-__device__ __forceinline__ void schur_update_tile(double* F, int ld, int m, int k, double d0, double d1, double d2) {
+// G x G thread grid, MR row/column blocks per thread, operand columns cached in registers.
+template <int G, int MR, bool TWO, class S>
+__device__ __forceinline__ void schur_update_tile(const S& st, int m, int k, double d0, double d1, double d2) {
     const int ty = threadIdx.x / G, tx = threadIdx.x % G;
     const int r0 = k + (TWO ? 2 : 1);
     // number of G-row blocks of the trailing triangle: wave-uniform, so the unrolled loops below
@@ -280,10 +308,10 @@ __device__ __forceinline__ void schur_update_tile(double* F, int ld, int m, int 
         if (a >= nb) break;
         const int i = r0 + ty + G * a;
         const int j = r0 + tx + G * a;
-        ci0[a] = i < m ? F[i * ld + k] : 0.0;
-        ci1[a] = (TWO && i < m) ? F[i * ld + k + 1] : 0.0;
-        const double x0 = j < m ? F[j * ld + k] : 0.0;
-        const double x1 = (TWO && j < m) ? F[j * ld + k + 1] : 0.0;
+        ci0[a] = i < m ? st.at(i, k) : 0.0;
+        ci1[a] = (TWO && i < m) ? st.at(i, k + 1) : 0.0;
+        const double x0 = j < m ? st.at(j, k) : 0.0;
+        const double x1 = (TWO && j < m) ? st.at(j, k + 1) : 0.0;
         if (TWO) {  // [l0 l1] = [x0 x1] * inv([[d0 d1][d1 d2]]) with d pre-divided by det
             lj0[a] = d2 * x0 - d1 * x1;
             lj1[a] = d0 * x1 - d1 * x0;
@@ -301,7 +329,7 @@ __device__ __forceinline__ void schur_update_tile(double* F, int ld, int m, int 
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
             const int j = r0 + tx + G * b;
-            acc[b] = (i < m && j <= i) ? F[i * ld + j] : 0.0;
+            acc[b] = (i < m && j <= i) ? st.at(i, j) : 0.0;
         }
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
@@ -312,29 +340,29 @@ __device__ __forceinline__ void schur_update_tile(double* F, int ld, int m, int 
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
             const int j = r0 + tx + G * b;
-            if (i < m && j <= i) F[i * ld + j] = acc[b];
+            if (i < m && j <= i) st.at(i, j) = acc[b];
         }
     }
 }
 
-// generic (global-memory) Schur update, any m
-template <int G, bool TWO>
-__device__ void schur_update_generic(double* F, int ld, int m, int k, double d0, double d1, double d2) {
+// generic Schur update, any m (fronts in HBM scratch)
+template <int G, bool TWO, class S>
+__device__ void schur_update_generic(const S& st, int m, int k, double d0, double d1, double d2) {
     const int ty = threadIdx.x / G, tx = threadIdx.x % G;
     const int r0 = k + (TWO ? 2 : 1);
     for (int i = r0 + ty; i < m; i += G) {
-        const double a0 = F[i * ld + k];
-        const double a1 = TWO ? F[i * ld + k + 1] : 0.0;
+        const double a0 = st.at(i, k);
+        const double a1 = TWO ? st.at(i, k + 1) : 0.0;
         for (int j = r0 + tx; j <= i; j += G) {
-            const double x0 = F[j * ld + k];
+            const double x0 = st.at(j, k);
             double upd;
             if (TWO) {
-                const double x1 = F[j * ld + k + 1];
+                const double x1 = st.at(j, k + 1);
                 upd = a0 * (d2 * x0 - d1 * x1) + a1 * (d0 * x1 - d1 * x0);
             } else {
                 upd = a0 * (x0 * d0);
             }
-            F[i * ld + j] -= upd;
+            st.at(i, j) -= upd;
         }
     }
 }
@@ -344,10 +372,10 @@ struct FrontShared {
     int stuck;
 };
 
-// Factor one front whose lower triangle is in F (ld), fully-summed columns 0..p-1.
+// Factor one front (lower triangle in st), fully-summed columns 0..p-1.
 // Writes L (packed trapezoid), pivot kinds, permuted row ids, CB, inertia counters.
-template <int NT, int MR>
-__device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
+template <int NT, int MR, class S>
+__device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
                              double* coefA, double* coefB, const FactorArgs& A, int f, FrontShared* sh) {
     const int tid = threadIdx.x;
     for (int i = tid; i < m; i += NT) lorig[i] = i;  // local position before pivoting
@@ -355,11 +383,15 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
     const double thres = DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits);
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
     bool delays_recorded = false;
-    auto lorig_var = [&](int q) { return lrow[q]; };
     int k = 0;
     while (k < p) {
         if (tid < 64) {
-            PivotDecision d = search_pivot(F, ld, m, k, p, A.u, thres);
+            PivotDecision d;
+            if (quick_1x1(st, m, k, A.u, thres)) {
+                d = PivotDecision{PIV_1X1, k, -1, 0};
+            } else {
+                d = search_pivot(st, m, k, p, A.u, thres);
+            }
             if (tid == 0) {
                 sh->dec = d;
                 if (A.stamps) { A.stamps[8 * f + 4] += (unsigned long long)(d.c - k + 1); A.stamps[8 * f + 5] += 1; }
@@ -369,13 +401,13 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
         PivotDecision d = sh->dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
-            sym_swap<NT>(F, ld, m, k, d.c, lrow, lorig);
+            sym_swap<NT>(st, m, k, d.c, lrow, lorig);
             __syncthreads();
         }
         if (d.kind == PIV_2X2_A) {
             int r = d.r == k ? d.c : d.r;
             if (r != k + 1) {
-                sym_swap<NT>(F, ld, m, k + 1, r, lrow, lorig);
+                sym_swap<NT>(st, m, k + 1, r, lrow, lorig);
                 __syncthreads();
             }
         }
@@ -387,28 +419,28 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
             if (d.relaxed && !delays_recorded && A.record_delays && A.fparent[f] >= 0) {
                 delays_recorded = true;
                 unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
-                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lorig_var(q);
+                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
             }
         }
         if (d.kind == PIV_NULL) {
-            for (int i = k + 1 + tid; i < m; i += NT) F[i * ld + k] = 0.0;
+            for (int i = k + 1 + tid; i < m; i += NT) st.at(i, k) = 0.0;
             if (tid == 0) { piv[k] = PIV_NULL; nzero++; }
             __syncthreads();
             k += 1;
         } else if (d.kind == PIV_1X1) {
-            const double dk = F[k * ld + k];
+            const double dk = st.at(k, k);
             const double dinv = 1.0 / dk;
-            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), false>(F, ld, m, k, dinv, 0.0, 0.0);
-            else schur_update_generic<kGrid<NT>, false>(F, ld, m, k, dinv, 0.0, 0.0);
+            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), false>(st, m, k, dinv, 0.0, 0.0);
+            else schur_update_generic<kGrid<NT>, false>(st, m, k, dinv, 0.0, 0.0);
             if (tid == 0) { piv[k] = PIV_1X1; if (dk > 0.0) npos++; else nneg++; }
             __syncthreads();
             k += 1;
         } else {  // 2x2
-            const double a = F[k * ld + k], b = F[(k + 1) * ld + k], e = F[(k + 1) * ld + k + 1];
+            const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
             const double det = a * e - b * b;
             const double idet = 1.0 / det;
-            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), true>(F, ld, m, k, a * idet, b * idet, e * idet);
-            else schur_update_generic<kGrid<NT>, true>(F, ld, m, k, a * idet, b * idet, e * idet);
+            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), true>(st, m, k, a * idet, b * idet, e * idet);
+            else schur_update_generic<kGrid<NT>, true>(st, m, k, a * idet, b * idet, e * idet);
             if (tid == 0) {
                 piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; n2++;
                 if (det < 0.0) { npos++; nneg++; }
@@ -422,15 +454,15 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
     if (A.stamps && tid == 0) A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
     // ---- write L: packed lower trapezoid, column j rows j..m-1 ----
     // per-column coefficients first (one division per column, not per entry):
-    // L(i,j) = cA[j] * F[i][base] + cB[j] * F[i][base+1], base = j (1x1, 2x2 first) or j-1 (2x2 second)
+    // L(i,j) = cA[j] * A(i,base) + cB[j] * A(i,base+1), base = j (1x1, 2x2 first) or j-1 (2x2 second)
     for (int j = tid; j < p; j += NT) {
         const int8_t kind = piv[j];
         double ca = 0.0, cbv = 0.0;
         if (kind == PIV_1X1) {
-            ca = 1.0 / F[j * ld + j];
+            ca = 1.0 / st.at(j, j);
         } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
             const int k0 = kind == PIV_2X2_A ? j : j - 1;
-            const double a = F[k0 * ld + k0], b = F[(k0 + 1) * ld + k0], e = F[(k0 + 1) * ld + k0 + 1];
+            const double a = st.at(k0, k0), b = st.at(k0 + 1, k0), e = st.at(k0 + 1, k0 + 1);
             const double idet = 1.0 / (a * e - b * b);
             if (kind == PIV_2X2_A) { ca = e * idet; cbv = -b * idet; }
             else { ca = -b * idet; cbv = a * idet; }
@@ -451,13 +483,13 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
             const int8_t kind = piv[j];
             double v;
             if (i == j) {
-                v = kind == PIV_NULL ? 0.0 : F[j * ld + j];
+                v = kind == PIV_NULL ? 0.0 : st.at(j, j);
             } else if (kind == PIV_2X2_A && i == j + 1) {
-                v = F[(j + 1) * ld + j];  // D off-diagonal
+                v = st.at(j + 1, j);  // D off-diagonal
             } else {
                 const int base = kind == PIV_2X2_B ? j - 1 : j;
-                v = coefA[j] * F[i * ld + base];
-                if (kind >= PIV_2X2_A) v += coefB[j] * F[i * ld + base + 1];
+                v = coefA[j] * st.at(i, base);
+                if (kind >= PIV_2X2_A) v += coefB[j] * st.at(i, base + 1);
             }
             L[t] = v;
         }
@@ -479,7 +511,7 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
         for (int64_t t = tid; t < ctot; t += NT) {
             while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
             const int i = j + (int)(t - cs);
-            cb[t] = F[(p + i) * ld + (p + j)];
+            cb[t] = st.at(p + i, p + j);
         }
     }
     if (tid == 0) {
@@ -493,9 +525,9 @@ __device__ void factor_front(double* F, int ld, int m, int p, int32_t* lrow, int
     }
 }
 
-// assemble original entries and children contribution blocks into F (zeroed lower triangle)
-template <int NT>
-__device__ void assemble_front(double* F, int ld, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
+// assemble original entries and children contribution blocks into the (zeroed) front
+template <int NT, class S>
+__device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
                                const FactorArgs& A, int f) {
     const int tid = threadIdx.x;
     const int64_t ro = A.rows_off[f];
@@ -504,15 +536,12 @@ __device__ void assemble_front(double* F, int ld, int m, int p, int32_t* lrow, d
         lrow[i] = v;
         sloc[i] = A.scale[v];
     }
-    for (int i = tid; i < m; i += NT) {
-        double* Fi = F + (int64_t)i * ld;
-        for (int j = 0; j <= i; ++j) Fi[j] = 0.0;
-    }
+    for (int64_t t = tid; t < fsize; t += NT) st.F[t] = 0.0;
     __syncthreads();
     for (int64_t e = A.ent_off[f] + tid; e < A.ent_off[f + 1]; e += NT) {
         const uint32_t lp = A.ent_lpos[e];
         const int lr = (int)(lp >> 16), lc = (int)(lp & 0xffffu);
-        F[lr * ld + lc] = sloc[lr] * A.uval[e] * sloc[lc];
+        st.at(lr, lc) = sloc[lr] * A.uval[e] * sloc[lc];
     }
     for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
         const int cm = A.ch_cm[ci];  // child metadata stored with the edge: one load, no chain
@@ -539,21 +568,25 @@ __device__ void assemble_front(double* F, int ld, int m, int p, int32_t* lrow, d
                 const int64_t t = t0 + (int64_t)q * NT;
                 if (t < ctot) {
                     while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
-                    pos[q] = rstage[j + (int)(t - cs)] * ld + rstage[j];
+                    pos[q] = st.idx(rstage[j + (int)(t - cs)], rstage[j]);
                 } else {
                     pos[q] = -1;
                 }
             }
             double old[B];
 #pragma unroll
-            for (int q = 0; q < B; ++q) old[q] = pos[q] >= 0 ? F[pos[q]] : 0.0;
+            for (int q = 0; q < B; ++q) old[q] = pos[q] >= 0 ? st.F[pos[q]] : 0.0;
 #pragma unroll
             for (int q = 0; q < B; ++q)
-                if (pos[q] >= 0) F[pos[q]] = old[q] + v[q];
+                if (pos[q] >= 0) st.F[pos[q]] = old[q] + v[q];
         }
     }
     __syncthreads();
 }
+
+// LDS layout of one front: [FrontShared 32 B][packed lower m(m+1)/2, even][sloc m][coefB m]
+// [lrow m][rstage/lorig m][piv m]
+__device__ __forceinline__ int64_t packed_even(int m) { return (((int64_t)m * (m + 1) / 2) + 1) & ~1ll; }
 
 template <int NT, int MR>
 __global__ __launch_bounds__(NT) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
@@ -561,17 +594,17 @@ __global__ __launch_bounds__(NT) void k_factor_lds(FactorArgs A, const int32_t* 
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
     const int f = fronts[blockIdx.x];
     const int m = A.fm[f], p = A.fp[f];
-    const int ld = m | 1;
-    double* F = smem + 4;
-    double* sloc = F + (int64_t)ld * m;
+    const PackedStore st{smem + 4};
+    const int64_t fsize = packed_even(m);
+    double* sloc = smem + 4 + fsize;
     double* coefB = sloc + m;
     int32_t* lrow = (int32_t*)(coefB + m);
     int32_t* rstage = lrow + m;
     int8_t* pk = (int8_t*)(rstage + m);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
-    assemble_front<NT>(F, ld, m, p, lrow, sloc, rstage, A, f);
+    assemble_front<NT>(st, fsize, m, p, lrow, sloc, rstage, A, f);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front<NT, MR>(F, ld, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    factor_front<NT, MR>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -580,15 +613,14 @@ __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const 
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
     const int f = fronts[blockIdx.x];
     const int m = A.fm[f], p = A.fp[f];
-    const int ld = m;
-    double* F = A.gscratch + A.gscratch_off[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
     double* sloc = smem + 4;
     double* coefB = sloc + m;
     int32_t* lrow = (int32_t*)(coefB + m);
     int32_t* rstage = lrow + m;
     int8_t* pk = (int8_t*)(rstage + m);
-    assemble_front<kThreads>(F, ld, m, p, lrow, sloc, rstage, A, f);
-    factor_front<kThreads, 0>(F, ld, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    assemble_front<kThreads>(st, (int64_t)m * m, m, p, lrow, sloc, rstage, A, f);
+    factor_front<kThreads, 0>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -819,8 +851,8 @@ hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hip
 }
 
 size_t factor_lds_bytes(int mmax) {
-    int ld = mmax | 1;
-    return 32 + (size_t)ld * mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
+    const size_t packed = (((size_t)mmax * (mmax + 1) / 2) + 1) & ~(size_t)1;
+    return 32 + packed * sizeof(double) + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
            (size_t)((mmax + 15) & ~15);
 }
 
