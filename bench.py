@@ -38,6 +38,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-n", type=int, default=1_000_000)
     ap.add_argument("--profile-only", action="store_true", help="skip event pass and CPU baseline")
+    ap.add_argument("--leaf", type=int, default=0, help="nested-dissection leaf size (0 = library default)")
+    ap.add_argument("--block", type=int, default=0, help="max supernode width (0 = library default)")
     return ap.parse_args()
 
 
@@ -59,6 +61,10 @@ def main():
     seed = uno_amd.SEEDS["C3"] + rank  # independent system per rank
     n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(args.n, seed)
     kkt = uno_amd.HipKKT(local)
+    if args.leaf:
+        kkt.set_option("leaf_size", args.leaf)
+    if args.block:
+        kkt.set_option("max_block", args.block)
     t0 = time.perf_counter()
     kkt.analyze(n, rows, cols)
     t_analysis = time.perf_counter() - t0

@@ -22,9 +22,10 @@ st = out.reshape(nf, 8).astype(np.int64)
 asm = (st[:, 1] - st[:, 0]) * 10e-3   # us
 loop = (st[:, 2] - st[:, 1]) * 10e-3
 wout = (st[:, 3] - st[:, 2]) * 10e-3
-cand = st[:, 4]; steps = st[:, 5]
+cs = st[:, 4]; cu = st[:, 5]; cr = st[:, 6]; steps = np.maximum(st[:, 7], 1)
 print("fronts", nf, "levels", fl.max() + 1)
 for lev in range(fl.max() + 1):
     s = fl == lev
     print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} p {fp[s].mean():5.1f} | assemble {asm[s].mean():7.2f} us "
-          f"loop {loop[s].mean():7.2f} us ({loop[s].mean()/max(1,steps[s].mean()):.3f} us/step, cand/step {cand[s].sum()/max(1,steps[s].sum()):.2f}) write {wout[s].mean():6.2f} us")
+          f"loop {loop[s].mean():7.2f} us write {wout[s].mean():6.2f} us | cycles/step search {(cs[s]/steps[s]).mean():7.0f} "
+          f"update {(cu[s]/steps[s]).mean():7.0f} rest {(cr[s]/steps[s]).mean():6.0f}")

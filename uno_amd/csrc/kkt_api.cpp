@@ -218,7 +218,7 @@ int upload_structure(uno_kkt_t h) {
     const int64_t n = S.n;
     // global scratch for fronts too large for LDS
     std::vector<int64_t> goff(S.nf + 1, 0);
-    int64_t gtot = 0;
+    int64_t gtot = 8;  // leading pad: element -1 of the first front is the kernels' trash slot
     for (int64_t f = 0; f < S.nf; ++f) {
         goff[f] = gtot;
         if (S.f_m[f] > kMaxLdsFront) gtot += (int64_t)S.f_m[f] * S.f_m[f];

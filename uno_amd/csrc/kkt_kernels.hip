@@ -302,16 +302,26 @@ __device__ __forceinline__ void schur_update_tile(const S& st, int m, int k, dou
     // number of G-row blocks of the trailing triangle: wave-uniform, so the unrolled loops below
     // branch out (s_cbranch) instead of issuing masked-off work for empty blocks
     const int nb = (m - r0 + G - 1) / G;
+    // Branch-free element access: a lane outside the triangle reads/writes the trash slot st.F[-1]
+    // (reserved in the LDS layout); guarded accesses would compile to one divergent branch per
+    // element and serialise every LDS access with its full latency.
     double ci0[MR], ci1[MR], lj0[MR], lj1[MR];
+    int rb[MR];  // offset of A(i, 0) for this thread's rows (one multiply per row, not per element)
 #pragma unroll
     for (int a = 0; a < MR; ++a) {
         if (a >= nb) break;
         const int i = r0 + ty + G * a;
         const int j = r0 + tx + G * a;
-        ci0[a] = i < m ? st.at(i, k) : 0.0;
-        ci1[a] = (TWO && i < m) ? st.at(i, k + 1) : 0.0;
-        const double x0 = j < m ? st.at(j, k) : 0.0;
-        const double x1 = (TWO && j < m) ? st.at(j, k + 1) : 0.0;
+        rb[a] = st.idx(i, 0);
+        const int ai = i < m ? rb[a] + k : -1;
+        const int aj = j < m ? st.idx(j, k) : -1;
+        ci0[a] = st.F[ai];
+        const double x0 = st.F[aj];
+        double x1 = 0.0;
+        if (TWO) {
+            ci1[a] = st.F[i < m ? ai + 1 : -1];
+            x1 = st.F[j < m ? aj + 1 : -1];
+        }
         if (TWO) {  // [l0 l1] = [x0 x1] * inv([[d0 d1][d1 d2]]) with d pre-divided by det
             lj0[a] = d2 * x0 - d1 * x1;
             lj1[a] = d0 * x1 - d1 * x0;
@@ -325,11 +335,13 @@ __device__ __forceinline__ void schur_update_tile(const S& st, int m, int k, dou
     for (int a = 0; a < MR; ++a) {
         if (a >= nb) break;
         const int i = r0 + ty + G * a;
+        int addr[MR];
         double acc[MR];
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
             const int j = r0 + tx + G * b;
-            acc[b] = (i < m && j <= i) ? st.at(i, j) : 0.0;
+            addr[b] = (i < m && j <= i) ? rb[a] + j : -1;
+            acc[b] = st.F[addr[b]];
         }
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
@@ -338,10 +350,7 @@ __device__ __forceinline__ void schur_update_tile(const S& st, int m, int k, dou
             acc[b] -= upd;
         }
 #pragma unroll
-        for (int b = 0; b <= a; ++b) {
-            const int j = r0 + tx + G * b;
-            if (i < m && j <= i) st.at(i, j) = acc[b];
-        }
+        for (int b = 0; b <= a; ++b) st.F[addr[b]] = acc[b];
     }
 }
 
@@ -383,8 +392,12 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     const double thres = DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits);
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
     bool delays_recorded = false;
+    // diagnostics (stamps build path only): shader-clock cycles spent in search / update / rest
+    unsigned long long cyc_search = 0, cyc_update = 0, cyc_rest = 0, t_mark = 0;
+    const bool stamping = A.stamps != nullptr;
     int k = 0;
     while (k < p) {
+        if (stamping) t_mark = __builtin_amdgcn_s_memtime();
         if (tid < 64) {
             PivotDecision d;
             if (quick_1x1(st, m, k, A.u, thres)) {
@@ -392,12 +405,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             } else {
                 d = search_pivot(st, m, k, p, A.u, thres);
             }
-            if (tid == 0) {
-                sh->dec = d;
-                if (A.stamps) { A.stamps[8 * f + 4] += (unsigned long long)(d.c - k + 1); A.stamps[8 * f + 5] += 1; }
-            }
+            if (tid == 0) sh->dec = d;
         }
         __syncthreads();
+        if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
         PivotDecision d = sh->dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
@@ -430,10 +441,12 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         } else if (d.kind == PIV_1X1) {
             const double dk = st.at(k, k);
             const double dinv = 1.0 / dk;
+            if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_rest += t - t_mark; t_mark = t; }
             if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), false>(st, m, k, dinv, 0.0, 0.0);
             else schur_update_generic<kGrid<NT>, false>(st, m, k, dinv, 0.0, 0.0);
             if (tid == 0) { piv[k] = PIV_1X1; if (dk > 0.0) npos++; else nneg++; }
             __syncthreads();
+            if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; t_mark = t; }
             k += 1;
         } else {  // 2x2
             const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
@@ -451,7 +464,13 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             k += 2;
         }
     }
-    if (A.stamps && tid == 0) A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
+    if (A.stamps && tid == 0) {
+        A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
+        A.stamps[8 * f + 4] = cyc_search;
+        A.stamps[8 * f + 5] = cyc_update;
+        A.stamps[8 * f + 6] = cyc_rest;
+        A.stamps[8 * f + 7] = (unsigned long long)p;
+    }
     // ---- write L: packed lower trapezoid, column j rows j..m-1 ----
     // per-column coefficients first (one division per column, not per entry):
     // L(i,j) = cA[j] * A(i,base) + cB[j] * A(i,base+1), base = j (1x1, 2x2 first) or j-1 (2x2 second)
@@ -573,12 +592,12 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
                     pos[q] = -1;
                 }
             }
+            // branch-free: out-of-range lanes read/write the trash slot st.F[-1]
             double old[B];
 #pragma unroll
-            for (int q = 0; q < B; ++q) old[q] = pos[q] >= 0 ? st.F[pos[q]] : 0.0;
+            for (int q = 0; q < B; ++q) old[q] = st.F[pos[q]];
 #pragma unroll
-            for (int q = 0; q < B; ++q)
-                if (pos[q] >= 0) st.F[pos[q]] = old[q] + v[q];
+            for (int q = 0; q < B; ++q) st.F[pos[q]] = old[q] + v[q];
         }
     }
     __syncthreads();
