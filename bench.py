@@ -80,24 +80,8 @@ def main():
         kkt.solve_device(rhs_d.data_ptr(), x_d.data_ptr())
         return inertia
 
-    def barrier():
-        if world > 1:
-            dist.barrier()
-        torch.cuda.synchronize()
-
-    for _ in range(args.warmup):
-        inertia = step()
-    barrier()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        inertia = step()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    barrier()
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    elapsed = float(tmax.item())
+    from uno_amd.replicas import aggregate, timed_steps
+    elapsed, inertia = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, dev)
 
     # parity sanity on the measured system: relative residual of the last solve
     x = x_d.cpu().numpy()
@@ -123,9 +107,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    steps_total = args.steps * world
-    value = steps_total / elapsed
-    ms_per_step = 1e3 * elapsed / args.steps
+    value, ms_per_step = aggregate(args.steps, world, elapsed)
 
     # ---- roofline of the dominant kernel class ----
     K = args.steps

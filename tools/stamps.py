@@ -7,6 +7,8 @@ import uno_amd
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000000
 N, nv, m, r, c, v, b = uno_amd.arrowband(n, uno_amd.SEEDS["C3"])
 g = uno_amd.HipKKT(0)
+if os.environ.get("LEAF"):
+    g.set_option("leaf_size", int(os.environ["LEAF"]))
 g.analyze(N, r, c)
 g.factorize(v); g.inertia()
 g.set_option("stamps", 1)
@@ -28,4 +30,6 @@ for lev in range(fl.max() + 1):
     s = fl == lev
     print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} p {fp[s].mean():5.1f} | assemble {asm[s].mean():7.2f} us "
           f"loop {loop[s].mean():7.2f} us write {wout[s].mean():6.2f} us | cycles/step search {(cs[s]/steps[s]).mean():7.0f} "
-          f"update {(cu[s]/steps[s]).mean():7.0f} rest {(cr[s]/steps[s]).mean():6.0f}")
+          f"update {(cu[s]/steps[s]).mean():7.0f} rest {(cr[s]/steps[s]).mean():6.0f} | span {(st[s,3].max()-st[s,0].min())*10e-3:8.1f} us")
+tot = sum((st[fl == l, 3].max() - st[fl == l, 0].min()) * 10e-3 for l in range(fl.max() + 1))
+print(f"sum of level spans {tot:.1f} us")
