@@ -76,7 +76,7 @@ struct uno_kkt {
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
     DBuf<int32_t> ch_cm;
     DBuf<int8_t> piv;
-    DBuf<unsigned long long> anorm, counters, stamps;
+    DBuf<unsigned long long> anorm, counters, stamps, fcnt;
     int want_stamps = 0;
     DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed;
     int32_t n_long = 0;
@@ -256,6 +256,7 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->gscratch_off.upload(goff, s));
     HIPCHK(h, h->level_fronts.upload(S.level_fronts, s));
     HIPCHK(h, h->fstat.alloc(S.nf));
+    HIPCHK(h, h->fcnt.alloc(S.nf));
     HIPCHK(h, h->perm_d.upload(S.perm, s));
     HIPCHK(h, h->cptr.upload(S.cptr, s));
     HIPCHK(h, h->rptr.upload(S.rptr, s));
@@ -361,7 +362,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.ch_cm = h->ch_cm.p; A.ch_relmap_off = h->ch_relmap_off.p; A.ch_cb_off = h->ch_cb_off.p;
     A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
-    A.counters = h->counters.p; A.fstat = h->fstat.p; A.u = h->u; A.null_fac = h->null_fac;
+    A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     A.stamps = nullptr;
     if (h->want_stamps) {
@@ -373,6 +374,7 @@ int enqueue_factorization(uno_kkt_t h) {
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
         HIPCHK(h, launch_factor(A, h->level_fronts.p + L.begin, L.count, L.mmax, L.global, s));
     }
+    HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, S.nf, h->counters.p, s));
     HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     h->factor_enqueued = true;
     return UNO_KKT_OK;

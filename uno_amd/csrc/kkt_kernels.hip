@@ -535,12 +535,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     if (tid == 0) {
         A.fstat[f] = (int32_t)((nstuck > 0xffff ? 0xffff : nstuck) | ((nrel > 0x7fff ? 0x7fff : nrel) << 16));
-        atomicAdd((unsigned long long*)&A.counters[0], (unsigned long long)npos);
-        atomicAdd((unsigned long long*)&A.counters[1], (unsigned long long)nneg);
-        atomicAdd((unsigned long long*)&A.counters[2], (unsigned long long)nzero);
-        atomicAdd((unsigned long long*)&A.counters[3], (unsigned long long)n2);
-        atomicAdd((unsigned long long*)&A.counters[4], (unsigned long long)nrel);
-        atomicAdd((unsigned long long*)&A.counters[5], (unsigned long long)nstuck);
+        // per-front record instead of global atomics: thousands of fronts finishing together would
+        // serialize on the counters' cache line and stall every access routed to that L2 channel
+        A.fcnt[f] = (unsigned long long)npos | (unsigned long long)nneg << 16 | (unsigned long long)nzero << 32 |
+                    (unsigned long long)n2 << 48;
     }
 }
 
@@ -888,6 +886,38 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
         else if (mmax <= 64) hipLaunchKernelGGL((k_factor_lds<64, 8>), dim3(count), dim3(64), sh, s, A, fronts);
         else hipLaunchKernelGGL((k_factor_lds<kThreads, 8>), dim3(count), dim3(kThreads), sh, s, A, fronts);
     }
+    return hipGetLastError();
+}
+
+__global__ void __launch_bounds__(256) k_count(const unsigned long long* __restrict__ fcnt,
+                                               const int32_t* __restrict__ fstat, int64_t nf,
+                                               unsigned long long* __restrict__ counters) {
+    unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int64_t f = blockIdx.x * 256 + threadIdx.x; f < nf; f += (int64_t)gridDim.x * 256) {
+        const unsigned long long c = fcnt[f];
+        const uint32_t st = (uint32_t)fstat[f];
+        acc[0] += c & 0xffff; acc[1] += (c >> 16) & 0xffff; acc[2] += (c >> 32) & 0xffff; acc[3] += c >> 48;
+        acc[4] += st >> 16; acc[5] += st & 0xffff;
+    }
+    __shared__ unsigned long long red[6][4];
+#pragma unroll
+    for (int q = 0; q < 6; ++q) {
+        unsigned long long v = acc[q];
+        for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+        if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < 6) {
+        const unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
+        if (v) atomicAdd(counters + threadIdx.x, v);
+    }
+}
+
+hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, int64_t nf, unsigned long long* counters,
+                        hipStream_t s) {
+    if (nf <= 0) return hipSuccess;
+    const int blocks = (int)std::min<int64_t>(64, (nf + 255) / 256);
+    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, nf, counters);
     return hipGetLastError();
 }
 

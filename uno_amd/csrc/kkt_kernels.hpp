@@ -36,6 +36,7 @@ struct FactorArgs {
     int8_t* piv;                // pivot kinds (same layout as rows)
     unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck, delayed
     int32_t* fstat;             // per front: stuck pivots (low 16 bits) | relaxed pivots (high 16 bits)
+    unsigned long long* fcnt;   // per front: npos | nneg << 16 | nzero << 32 | n2x2 << 48 (summed by launch_count)
     const int32_t* fparent;     // assembly-tree parent (-1 = root)
     int32_t* delayed;           // original ids of columns that failed the threshold (counters[6] = count)
     int record_delays;
@@ -86,6 +87,9 @@ hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s);
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
+// counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
+hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, int64_t nf, unsigned long long* counters,
+                        hipStream_t s);
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
