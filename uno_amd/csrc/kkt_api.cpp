@@ -53,6 +53,13 @@ struct Launch {
     bool global;
 };
 
+// one solve launch: fronts solve_fronts[begin, begin+count) of one level; wave kernels (p <= 64,
+// m <= kMaxLdsFront) are grouped by the LDS their packed panel needs so small fronts keep occupancy
+struct SolveLaunch {
+    int level, begin, count, lds, mmax, pmax;
+    bool wave;
+};
+
 }  // namespace
 
 struct uno_kkt {
@@ -83,8 +90,8 @@ struct uno_kkt {
     int64_t max_long = 0;
     unsigned long long* h_counters = nullptr;
     std::vector<Launch> fac_launches;
-    std::vector<std::pair<int, int>> level_ranges;  // per level: begin, count (solve)
-    std::vector<int> level_mmax, level_pmax;
+    std::vector<SolveLaunch> sol_launches;  // ordered by level
+    DBuf<int32_t> solve_fronts;
     uno_kkt_stats_t st{};
     std::string err;
     // timing
@@ -294,16 +301,46 @@ int upload_structure(uno_kkt_t h) {
     }
     // launch plan: per level, fronts sorted by order (descending) -> size classes
     h->fac_launches.clear();
-    h->level_ranges.clear();
-    h->level_mmax.clear();
-    h->level_pmax.clear();
+    h->sol_launches.clear();
+    std::vector<int32_t> sfr;
+    sfr.reserve(S.nf);
     for (int l = 0; l < S.nlevels; ++l) {
         int b = S.level_off[l], e = S.level_off[l + 1];
-        h->level_ranges.push_back({b, e - b});
-        h->level_mmax.push_back(e > b ? S.f_m[S.level_fronts[b]] : 0);
-        int pm = 0;
-        for (int q = b; q < e; ++q) pm = std::max(pm, S.f_p[S.level_fronts[q]]);
-        h->level_pmax.push_back(pm);
+        {
+            std::vector<std::pair<int, int32_t>> wv;  // (LDS doubles, front)
+            std::vector<int32_t> big;
+            for (int q = b; q < e; ++q) {
+                const int32_t f = S.level_fronts[q];
+                const int m = S.f_m[f], p = S.f_p[f];
+                if (p <= 64 && m <= kMaxLdsFront) {
+                    const int sz = p * m - p * (p - 1) / 2;
+                    wv.push_back({((sz + 1) & ~1) + m, f});
+                } else {
+                    big.push_back(f);
+                }
+            }
+            std::sort(wv.begin(), wv.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+            size_t q = 0;
+            while (q < wv.size()) {
+                int cap = 256;
+                while (cap < wv[q].first) cap *= 2;
+                size_t r = q;
+                while (r < wv.size() && (wv[r].first > cap / 2 || cap == 256)) ++r;
+                SolveLaunch sl{l, (int)sfr.size(), (int)(r - q), wv[q].first, 0, 0, true};
+                for (size_t t = q; t < r; ++t) sfr.push_back(wv[t].second);
+                h->sol_launches.push_back(sl);
+                q = r;
+            }
+            if (!big.empty()) {
+                SolveLaunch sl{l, (int)sfr.size(), (int)big.size(), 0, 0, 0, false};
+                for (int32_t f : big) {
+                    sfr.push_back(f);
+                    sl.mmax = std::max(sl.mmax, S.f_m[f]);
+                    sl.pmax = std::max(sl.pmax, S.f_p[f]);
+                }
+                h->sol_launches.push_back(sl);
+            }
+        }
         int q = b;
         while (q < e) {
             int m0 = S.f_m[S.level_fronts[q]];
@@ -316,6 +353,7 @@ int upload_structure(uno_kkt_t h) {
             q = r;
         }
     }
+    HIPCHK(h, h->solve_fronts.upload(sfr, s));
     HIPCHK(h, hipStreamSynchronize(s));
     double an = h->st.analysis_seconds;
     int64_t nfac = h->st.factorizations, nsol = h->st.solves;
@@ -547,15 +585,18 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
     A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p;
-    for (int l = 0; l < S.nlevels; ++l) {
+    auto run = [&](const SolveLaunch& L, bool forward) -> hipError_t {
+        const int32_t* fr = h->solve_fronts.p + L.begin;
+        return L.wave ? launch_solve_wave(A, fr, L.count, L.lds, forward, s)
+                      : launch_solve(A, fr, L.count, L.mmax, L.pmax, forward, s);
+    };
+    for (size_t q = 0; q < h->sol_launches.size(); ++q) {
         TimerScope t(h, KC_SOLVE_FWD);
-        HIPCHK(h, launch_solve(A, h->level_fronts.p + h->level_ranges[l].first, h->level_ranges[l].second,
-                               h->level_mmax[l], h->level_pmax[l], true, s));
+        HIPCHK(h, run(h->sol_launches[q], true));
     }
-    for (int l = S.nlevels - 1; l >= 0; --l) {
+    for (size_t q = h->sol_launches.size(); q-- > 0;) {
         TimerScope t(h, KC_SOLVE_BWD);
-        HIPCHK(h, launch_solve(A, h->level_fronts.p + h->level_ranges[l].first, h->level_ranges[l].second,
-                               h->level_mmax[l], h->level_pmax[l], false, s));
+        HIPCHK(h, run(h->sol_launches[q], false));
     }
     double* xd = on_device ? x : h->bvec.p;
     {

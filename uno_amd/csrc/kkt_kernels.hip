@@ -818,6 +818,130 @@ __global__ __launch_bounds__(kThreads) void k_solve_bwd(SolveArgs A, const int32
     }
 }
 
+// One-wave solves for fronts with p <= 64 and m <= kMaxLdsFront (all but the rare dense fronts).
+// The front's packed L panel (column k rows k..m-1, SolveArgs::L_off) is copied into LDS in one flat
+// coalesced pass -- every load of the panel in flight at once instead of one round trip per column --
+// and the triangle, rectangle and diagonal then run from LDS: lane i owns row i of the triangle,
+// pivots are broadcast with readlane, no barriers beyond the staging one.
+__device__ __forceinline__ int pcol(int m, int k) { return k * m - k * (k - 1) / 2 - k; }  // P[pcol + i] = L(i,k)
+
+__device__ __forceinline__ void stage_panel(const double* __restrict__ L, int64_t Lo, int sz, double* P) {
+    const int lane = threadIdx.x;
+    int t = lane;
+    for (; t + 7 * 64 < sz; t += 8 * 64) {
+        double v[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[q] = L[Lo + t + q * 64];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) P[t + q * 64] = v[q];
+    }
+    for (; t < sz; t += 64) P[t] = L[Lo + t];
+}
+
+__global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int lane = threadIdx.x;
+    const int64_t ro = A.rows_off[f];
+    const int sz = p * m - p * (p - 1) / 2;
+    double* P = smem_s;
+    double* y = smem_s + ((sz + 1) & ~1);
+    const int mypiv = lane < p ? (int)A.piv[ro + lane] : 0;
+    for (int i = lane; i < m; i += 64) y[i] = i < p ? A.w[A.frow[ro + i]] : 0.0;
+    stage_panel(A.L, A.L_off[f], sz, P);
+    __syncthreads();
+    const int32_t* fpos = A.fpos + ro;  // this front's rows were permuted by pivoting
+    for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
+        const int c = A.child[ci];
+        const int cm = A.fm[c] - A.fp[c];
+        const int32_t* rm = A.relmap + A.relmap_off[c];
+        const double* cv = A.cvec + A.relmap_off[c];
+        for (int t = lane; t < cm; t += 64) y[fpos[rm[t]]] += cv[t];
+        __syncthreads();
+    }
+    // triangle
+    double yi = lane < p ? y[lane] : 0.0;
+    for (int k = 0; k < p; ++k) {
+        const int kind = __builtin_amdgcn_readlane(mypiv, k);
+        if (kind == PIV_1X1) {
+            const double yk = readlane_d(yi, k);
+            if (lane > k && lane < p) yi -= P[pcol(m, k) + lane] * yk;
+        } else if (kind == PIV_2X2_A) {
+            const double y0 = readlane_d(yi, k), y1 = readlane_d(yi, k + 1);
+            if (lane > k + 1 && lane < p) yi -= P[pcol(m, k) + lane] * y0 + P[pcol(m, k + 1) + lane] * y1;
+            ++k;
+        }
+    }
+    if (lane < p) y[lane] = yi;
+    __syncthreads();
+    // rectangle: contribution rows, handed to the parent
+    double* cvo = A.cvec + A.relmap_off[f];
+    for (int i = p + lane; i < m; i += 64) {
+        double acc = y[i];
+        int pc = 0;
+        for (int k = 0; k < p; ++k) {
+            acc -= P[pc + i] * y[k];
+            pc += m - k - 1;
+        }
+        cvo[i - p] = acc;
+    }
+    // block diagonal
+    if (lane < p) {
+        const int kind = mypiv;
+        double out = 0.0;  // null pivot contributes 0
+        if (kind == PIV_1X1) {
+            out = yi / P[pcol(m, lane) + lane];
+        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+            const int k0 = kind == PIV_2X2_A ? lane : lane - 1;
+            const double a = P[pcol(m, k0) + k0], b = P[pcol(m, k0) + k0 + 1];
+            const double e = P[pcol(m, k0 + 1) + k0 + 1];
+            const double det = a * e - b * b;
+            const double y0 = y[k0], y1 = y[k0 + 1];
+            out = kind == PIV_2X2_A ? (e * y0 - b * y1) / det : (a * y1 - b * y0) / det;
+        }
+        A.w[A.frow[ro + lane]] = out;
+    }
+}
+
+__global__ __launch_bounds__(64) void k_solve_bwd_w(SolveArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int lane = threadIdx.x;
+    const int64_t ro = A.rows_off[f];
+    const int sz = p * m - p * (p - 1) / 2;
+    double* P = smem_s;
+    double* x = smem_s + ((sz + 1) & ~1);
+    const int mypiv = lane < p ? (int)A.piv[ro + lane] : PIV_NULL;
+    for (int i = lane; i < m; i += 64) x[i] = A.w[A.frow[ro + i]];
+    stage_panel(A.L, A.L_off[f], sz, P);
+    __syncthreads();
+    // rectangle: lane k accumulates sum_{i>=p} L(i,k) x_i (x_i broadcast from LDS)
+    double xj = 0.0;
+    if (lane < p) {
+        const double* Pk = P + pcol(m, lane);
+        double s0 = 0.0, s1 = 0.0;
+        int i = p;
+        for (; i + 1 < m; i += 2) {
+            s0 += Pk[i] * x[i];
+            s1 += Pk[i + 1] * x[i + 1];
+        }
+        if (i < m) s0 += Pk[i] * x[i];
+        xj = x[lane];
+        if (mypiv != PIV_NULL) xj -= s0 + s1;
+    }
+    // triangle (transposed): lane j owns x_j
+    for (int k = p - 1; k >= 0; --k) {
+        const int kind = __builtin_amdgcn_readlane(mypiv, k);
+        if (kind == PIV_NULL) continue;
+        const double xk = readlane_d(xj, k);
+        const int skip = kind == PIV_2X2_B ? k - 1 : -1;
+        if (lane < k && lane != skip && mypiv != PIV_NULL) xj -= P[pcol(m, lane) + k] * xk;
+    }
+    if (lane < p) A.w[A.frow[ro + lane]] = xj;
+}
+
 // ------------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------------------
@@ -940,6 +1064,15 @@ hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, in
     size_t sh = (size_t)((mmax + 1) & ~1) * sizeof(double) + tri + 16;
     if (forward) hipLaunchKernelGGL(k_solve_fwd, dim3(count), dim3(kThreads), sh, s, A, fronts);
     else hipLaunchKernelGGL(k_solve_bwd, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int count, int lds_doubles, bool forward,
+                             hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    const size_t sh = (size_t)lds_doubles * sizeof(double) + 16;
+    if (forward) hipLaunchKernelGGL(k_solve_fwd_w, dim3(count), dim3(64), sh, s, A, fronts);
+    else hipLaunchKernelGGL(k_solve_bwd_w, dim3(count), dim3(64), sh, s, A, fronts);
     return hipGetLastError();
 }
 

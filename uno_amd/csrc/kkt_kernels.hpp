@@ -87,6 +87,10 @@ hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s);
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
+// one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of
+// p*m - p*(p-1)/2 (rounded up to even) + m
+hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int count, int lds_doubles, bool forward,
+                             hipStream_t s);
 // counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, int64_t nf, unsigned long long* counters,
                         hipStream_t s);
