@@ -376,6 +376,41 @@ __device__ void schur_update_generic(const S& st, int m, int k, double d0, doubl
     }
 }
 
+
+// ---- register-resident Schur complement (one-wave kernels, m <= 8*MR) ----
+// Lane (ty, tx) of an 8 x 8 grid owns A(i, j), i = ty + 8a, j = tx + 8b, b <= a < MR.  A pivot step
+// publishes column k to a 64-entry LDS vector, tests the pivot with one ballot and applies the
+// rank-1 update in registers: two LDS round trips per step instead of one per row block.  Steps
+// that need the full search (swaps, 2x2, null pivots) spill to the packed LDS front, run the
+// LDS code path, and reload; both paths do the same arithmetic on the same values.
+template <int MR, class S>
+__device__ __forceinline__ void reg_load(const S& st, int m, double (&R)[MR][MR]) {
+    const int ty = threadIdx.x >> 3, tx = threadIdx.x & 7;
+#pragma unroll
+    for (int a = 0; a < MR; ++a) {
+        const int i = ty + 8 * a;
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            const int j = tx + 8 * b;
+            R[a][b] = st.F[(i < m && j <= i) ? st.idx(i, j) : -1];
+        }
+    }
+}
+
+template <int MR, class S>
+__device__ __forceinline__ void reg_store(const S& st, int m, const double (&R)[MR][MR]) {
+    const int ty = threadIdx.x >> 3, tx = threadIdx.x & 7;
+#pragma unroll
+    for (int a = 0; a < MR; ++a) {
+        const int i = ty + 8 * a;
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            const int j = tx + 8 * b;
+            st.F[(i < m && j <= i) ? st.idx(i, j) : -1] = R[a][b];
+        }
+    }
+}
+
 struct FrontShared {
     PivotDecision dec;
     int stuck;
@@ -396,11 +431,67 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     unsigned long long cyc_search = 0, cyc_update = 0, cyc_rest = 0, t_mark = 0;
     const bool stamping = A.stamps != nullptr;
     int k = 0;
+    constexpr bool REG = NT == 64 && MR > 0;
+    constexpr int RM = MR > 0 ? MR : 1;
+    // register-resident path (see reg_load): the loop over column blocks is unrolled so the owner
+    // registers of column k (block k/8) are static; a step that fails the quick test spills, runs
+    // the LDS step below (search, interchanges, 1x1/2x2/null, Schur update) and reloads
+    double R[RM][RM];
+    double* colv = coefB;  // free until the write-out
+    if constexpr (REG) reg_load<RM>(st, m, R);
     while (k < p) {
+        if constexpr (REG) {
+            const int ty = tid >> 3, tx = tid & 7;
+            bool need = false;
+#pragma unroll
+            for (int bk = 0; bk < RM; ++bk) {
+                while (!need && k < p && (k >> 3) == bk) {
+                    if (stamping) t_mark = __builtin_amdgcn_s_memtime();
+                    const bool mine = tx == (k & 7);
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) {
+                        const int i = ty + 8 * a;
+                        double* dst = (mine && i >= k && i < m) ? colv + i : st.F - 1;
+                        *dst = R[a][bk];
+                    }
+                    __syncthreads();
+                    const double akk = colv[k];
+                    const int q = k + 1 + tid;
+                    const double x = colv[q < m ? q : m - 1];
+                    double lv[RM], cv[RM];
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) {
+                        const int i = ty + 8 * a, j = tx + 8 * a;
+                        const double vi = colv[i < m ? i : m - 1], vj = colv[j < m ? j : m - 1];
+                        lv[a] = (i > k && i < m) ? vi : 0.0;
+                        cv[a] = (j > k && j < m) ? vj : 0.0;
+                    }
+                    const double aak = fabs(akk);
+                    const bool bad = !(aak > thres) || (q < m && A.u * fabs(x) > aak);
+                    need = __ballot(bad) != 0;
+                    if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
+                    if (!need) {  // 1x1 pivot at k without interchange: rank-1 update in registers
+                        const double dinv = 1.0 / akk;
+#pragma unroll
+                        for (int b = bk; b < RM; ++b) cv[b] *= dinv;
+#pragma unroll
+                        for (int a = bk; a < RM; ++a)
+#pragma unroll
+                            for (int b = bk; b <= a; ++b) R[a][b] -= lv[a] * cv[b];
+                        if (tid == 0) { piv[k] = PIV_1X1; if (akk > 0.0) npos++; else nneg++; }
+                        if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; }
+                        k += 1;
+                    }
+                }
+            }
+            if (!need) break;
+            reg_store<RM>(st, m, R);
+            __syncthreads();
+        }
         if (stamping) t_mark = __builtin_amdgcn_s_memtime();
         if (tid < 64) {
             PivotDecision d;
-            if (quick_1x1(st, m, k, A.u, thres)) {
+            if (!REG && quick_1x1(st, m, k, A.u, thres)) {
                 d = PivotDecision{PIV_1X1, k, -1, 0};
             } else {
                 d = search_pivot(st, m, k, p, A.u, thres);
@@ -463,6 +554,11 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             __syncthreads();
             k += 2;
         }
+        if constexpr (REG) reg_load<RM>(st, m, R);
+    }
+    if constexpr (REG) {
+        reg_store<RM>(st, m, R);
+        __syncthreads();
     }
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
