@@ -149,6 +149,16 @@ __global__ void k_scale_update(const double* __restrict__ rmax, double* __restri
     }
 }
 
+// row-major packed lower triangle: t -> (r, c), t = r(r+1)/2 + c, 0 <= c <= r (t < 2^31)
+__device__ __forceinline__ void tri_rc(int t, int& r, int& c) {
+    int rr = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+    int s0 = (int)(((long long)rr * (rr + 1)) >> 1);
+    if (s0 > t) { s0 -= rr; --rr; }
+    else if (s0 + rr + 1 <= t) { s0 += rr + 1; ++rr; }
+    r = rr;
+    c = t - s0;
+}
+
 // ------------------------------------------------------------------------------------------------
 // dense front factorization
 // ------------------------------------------------------------------------------------------------
@@ -587,8 +597,25 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     __syncthreads();
     double* L = A.L + A.L_off[f];
-    const int64_t total = (int64_t)p * m - (int64_t)p * (p - 1) / 2;
-    {
+    if (NT == 64 && m <= 64) {
+        // one wave, m <= 64: column j is one coalesced store, lane = row offset from the diagonal
+        int64_t cs = 0;  // start of column j
+#pragma unroll 4
+        for (int j = 0; j < p; ++j) {
+            const int i = j + tid;
+            const int8_t kind = piv[j];
+            const int base = kind == PIV_2X2_B ? j - 1 : j;
+            const int ii = i < m ? i : m - 1;
+            const double x0 = st.at(ii, base), x1 = st.at(ii, base + (base + 1 < m ? 1 : 0));
+            double v = coefA[j] * x0;
+            if (kind >= PIV_2X2_A) v += coefB[j] * x1;
+            if (i == j) v = kind == PIV_NULL ? 0.0 : st.at(j, j);
+            else if (kind == PIV_2X2_A && i == j + 1) v = x0;  // D off-diagonal A(j+1, j)
+            if (i < m) L[cs + tid] = v;
+            cs += m - j;
+        }
+    } else {
+        const int64_t total = (int64_t)p * m - (int64_t)p * (p - 1) / 2;
         int j = 0;
         int64_t cs = 0;  // start of column j
 #pragma unroll 4
@@ -615,18 +642,16 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         A.fpos[A.rows_off[f] + lorig[i]] = i;  // analysis-order local row -> pivoted position
         if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
     }
-    // ---- contribution block: packed lower, column-major, order cm = m - p ----
+    // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
     const int cm = m - p;
     if (cm > 0) {
         double* cb = A.cb + A.cb_off[f];
-        const int64_t ctot = (int64_t)cm * (cm + 1) / 2;
-        int j = 0;
-        int64_t cs = 0;
+        const int ctot = cm * (cm + 1) / 2;
 #pragma unroll 4
-        for (int64_t t = tid; t < ctot; t += NT) {
-            while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
-            const int i = j + (int)(t - cs);
-            cb[t] = st.at(p + i, p + j);
+        for (int t = tid; t < ctot; t += NT) {
+            int r, c;
+            tri_rc(t, r, c);
+            cb[t] = st.at(p + r, p + c);
         }
     }
     if (tid == 0) {
@@ -638,12 +663,33 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
 }
 
-// assemble original entries and children contribution blocks into the (zeroed) front
+// assemble original entries and children contribution blocks into the (zeroed) front.
+// Latency-bound (a few KB per front), so the loads are grouped into as few dependent round trips as
+// possible: {rows, first entry batch, children's edge metadata} -> {scales} -> {per child: CB values
+// and both relmap entries of each element together}.
 template <int NT, class S>
 __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
                                const FactorArgs& A, int f) {
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
     const int64_t ro = A.rows_off[f];
+    const int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    const int c0 = A.child_off[f], c1 = A.child_off[f + 1];
+    constexpr int EB = 8;
+    uint32_t lp[EB];
+    double uv[EB];
+#pragma unroll
+    for (int q = 0; q < EB; ++q) {
+        const int64_t e = e0 + tid + (int64_t)q * NT;
+        lp[q] = e < e1 ? A.ent_lpos[e] : 0u;
+        uv[q] = e < e1 ? A.uval[e] : 0.0;
+    }
+    int my_cm = 0;
+    unsigned long long my_rmo = 0, my_cbo = 0;
+    if (lane < c1 - c0) {
+        my_cm = A.ch_cm[c0 + lane];
+        my_rmo = (unsigned long long)A.ch_relmap_off[c0 + lane];
+        my_cbo = (unsigned long long)A.ch_cb_off[c0 + lane];
+    }
     for (int i = tid; i < m; i += NT) {
         const int32_t v = A.rows[ro + i];
         lrow[i] = v;
@@ -651,47 +697,63 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
     }
     for (int64_t t = tid; t < fsize; t += NT) st.F[t] = 0.0;
     __syncthreads();
-    for (int64_t e = A.ent_off[f] + tid; e < A.ent_off[f + 1]; e += NT) {
-        const uint32_t lp = A.ent_lpos[e];
-        const int lr = (int)(lp >> 16), lc = (int)(lp & 0xffffu);
-        st.at(lr, lc) = sloc[lr] * A.uval[e] * sloc[lc];
+    // original entries (distinct positions, summed duplicates already packed by k_pack)
+    for (int64_t eb = e0 + tid;; eb += (int64_t)EB * NT) {
+#pragma unroll
+        for (int q = 0; q < EB; ++q) {
+            const int64_t e = eb + (int64_t)q * NT;
+            const int lr = (int)(lp[q] >> 16), lc = (int)(lp[q] & 0xffffu);
+            const double v = sloc[lr] * uv[q] * sloc[lc];
+            st.F[e < e1 ? st.idx(lr, lc) : -1] = v;
+        }
+        const int64_t nb = eb + (int64_t)EB * NT;
+        if (nb - tid >= e1) break;  // uniform
+#pragma unroll
+        for (int q = 0; q < EB; ++q) {
+            const int64_t e = nb + (int64_t)q * NT;
+            lp[q] = e < e1 ? A.ent_lpos[e] : 0u;
+            uv[q] = e < e1 ? A.uval[e] : 0.0;
+        }
     }
-    for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
-        const int cm = A.ch_cm[ci];  // child metadata stored with the edge: one load, no chain
-        if (cm <= 0) continue;
-        __syncthreads();  // previous child's adds done, rstage free
-        const int32_t* rm = A.relmap + A.ch_relmap_off[ci];
-        for (int i = tid; i < cm; i += NT) rstage[i] = rm[i];
-        __syncthreads();
-        const double* cb = A.cb + A.ch_cb_off[ci];
-        const int64_t ctot = (int64_t)cm * (cm + 1) / 2;
-        int j = 0;
-        int64_t cs = 0;
-        constexpr int B = 8;  // batch: issue B global loads before the dependent LDS updates
-        for (int64_t t0 = tid; t0 < ctot; t0 += (int64_t)NT * B) {
-            double v[B];
-            int pos[B];
+    // children: contribution blocks are row-major packed lower triangles (row r: columns 0..r);
+    // relmap maps child CB rows to ascending parent rows, so (rm[r], rm[c]) is in the lower triangle
+    constexpr int CB = 8;
+    for (int cb0 = c0; cb0 < c1; cb0 += 64) {
+        if (cb0 != c0 && lane < c1 - cb0) {
+            my_cm = A.ch_cm[cb0 + lane];
+            my_rmo = (unsigned long long)A.ch_relmap_off[cb0 + lane];
+            my_cbo = (unsigned long long)A.ch_cb_off[cb0 + lane];
+        }
+        const int nc = c1 - cb0 < 64 ? c1 - cb0 : 64;
+        for (int q = 0; q < nc; ++q) {
+            const int cm = __builtin_amdgcn_readlane(my_cm, q);
+            if (cm <= 0) continue;
+            const int32_t* rm = A.relmap + (int64_t)readlane64(my_rmo, q);
+            const double* cb = A.cb + (int64_t)readlane64(my_cbo, q);
+            const int ctot = cm * (cm + 1) / 2;
+            for (int t0 = tid; t0 < ctot; t0 += NT * CB) {
+                double v[CB];
+                int32_t gi[CB], gj[CB];
 #pragma unroll
-            for (int q = 0; q < B; ++q) {
-                const int64_t t = t0 + (int64_t)q * NT;
-                v[q] = t < ctot ? cb[t] : 0.0;
-            }
-#pragma unroll
-            for (int q = 0; q < B; ++q) {
-                const int64_t t = t0 + (int64_t)q * NT;
-                if (t < ctot) {
-                    while (t >= cs + (cm - j)) { cs += cm - j; ++j; }
-                    pos[q] = st.idx(rstage[j + (int)(t - cs)], rstage[j]);
-                } else {
-                    pos[q] = -1;
+                for (int u = 0; u < CB; ++u) {
+                    const int t = t0 + u * NT;
+                    int r = 0, c = 0;
+                    if (t < ctot) tri_rc(t, r, c);
+                    v[u] = t < ctot ? cb[t] : 0.0;
+                    gi[u] = rm[r];
+                    gj[u] = rm[c];
                 }
+                int pos[CB];
+                double old[CB];
+#pragma unroll
+                for (int u = 0; u < CB; ++u) {
+                    pos[u] = t0 + u * NT < ctot ? st.idx(gi[u], gj[u]) : -1;
+                    old[u] = st.F[pos[u]];
+                }
+#pragma unroll
+                for (int u = 0; u < CB; ++u) st.F[pos[u]] = old[u] + v[u];
             }
-            // branch-free: out-of-range lanes read/write the trash slot st.F[-1]
-            double old[B];
-#pragma unroll
-            for (int q = 0; q < B; ++q) old[q] = st.F[pos[q]];
-#pragma unroll
-            for (int q = 0; q < B; ++q) st.F[pos[q]] = old[q] + v[q];
+            if (NT > 64) __syncthreads();  // children may overlap: one child at a time
         }
     }
     __syncthreads();
