@@ -387,35 +387,41 @@ __device__ void schur_update_generic(const S& st, int m, int k, double d0, doubl
 }
 
 
-// ---- register-resident Schur complement (one-wave kernels, m <= 8*MR) ----
-// Lane (ty, tx) of an 8 x 8 grid owns A(i, j), i = ty + 8a, j = tx + 8b, b <= a < MR.  A pivot step
-// publishes column k to a 64-entry LDS vector, tests the pivot with one ballot and applies the
+// ---- register-resident Schur complement (LDS fronts, m <= G*MR) ----
+// Thread (ty, tx) of a G x G grid owns A(i, j), i = ty + G a, j = tx + G b, b <= a < MR.  A pivot
+// step publishes column k to an LDS vector, tests the pivot (one ballot per wave) and applies the
 // rank-1 update in registers: two LDS round trips per step instead of one per row block.  Steps
 // that need the full search (swaps, 2x2, null pivots) spill to the packed LDS front, run the
 // LDS code path, and reload; both paths do the same arithmetic on the same values.
-template <int MR, class S>
+template <int G, int MR, class S>
 __device__ __forceinline__ void reg_load(const S& st, int m, double (&R)[MR][MR]) {
-    const int ty = threadIdx.x >> 3, tx = threadIdx.x & 7;
+    int ty = threadIdx.x / G, tx = threadIdx.x % G;
+    // opaque coordinates: keeps the 36 element addresses from being hoisted into live registers
+    // across the whole pivot loop (this runs once per front plus once per fallback step)
+    asm volatile("" : "+v"(ty), "+v"(tx));
 #pragma unroll
     for (int a = 0; a < MR; ++a) {
-        const int i = ty + 8 * a;
+        const int i = ty + G * a;
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
-            const int j = tx + 8 * b;
+            const int j = tx + G * b;
             R[a][b] = st.F[(i < m && j <= i) ? st.idx(i, j) : -1];
         }
     }
 }
 
-template <int MR, class S>
+template <int G, int MR, class S>
 __device__ __forceinline__ void reg_store(const S& st, int m, const double (&R)[MR][MR]) {
-    const int ty = threadIdx.x >> 3, tx = threadIdx.x & 7;
+    int ty = threadIdx.x / G, tx = threadIdx.x % G;
+    // opaque coordinates: keeps the 36 element addresses from being hoisted into live registers
+    // across the whole pivot loop (this runs once per front plus once per fallback step)
+    asm volatile("" : "+v"(ty), "+v"(tx));
 #pragma unroll
     for (int a = 0; a < MR; ++a) {
-        const int i = ty + 8 * a;
+        const int i = ty + G * a;
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
-            const int j = tx + 8 * b;
+            const int j = tx + G * b;
             st.F[(i < m && j <= i) ? st.idx(i, j) : -1] = R[a][b];
         }
     }
@@ -424,6 +430,7 @@ __device__ __forceinline__ void reg_store(const S& st, int m, const double (&R)[
 struct FrontShared {
     PivotDecision dec;
     int stuck;
+    int failk;  // register path, several waves: last step whose quick pivot test failed in some wave
 };
 
 // Factor one front (lower triangle in st), fully-summed columns 0..p-1.
@@ -441,44 +448,68 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     unsigned long long cyc_search = 0, cyc_update = 0, cyc_rest = 0, t_mark = 0;
     const bool stamping = A.stamps != nullptr;
     int k = 0;
-    constexpr bool REG = NT == 64 && MR > 0;
+    constexpr bool REG = MR > 0;
     constexpr int RM = MR > 0 ? MR : 1;
+    constexpr int G = kGrid<NT>;
+    constexpr int W = NT / 64;
     // register-resident path (see reg_load): the loop over column blocks is unrolled so the owner
-    // registers of column k (block k/8) are static; a step that fails the quick test spills, runs
+    // registers of column k (block k/G) are static; a step that fails the quick test spills, runs
     // the LDS step below (search, interchanges, 1x1/2x2/null, Schur update) and reloads
     double R[RM][RM];
     double* colv = coefB;  // free until the write-out
-    if constexpr (REG) reg_load<RM>(st, m, R);
+    if constexpr (REG) {
+        if (W > 1 && tid == 0) sh->failk = -1;
+        reg_load<G, RM>(st, m, R);
+    }
     while (k < p) {
         if constexpr (REG) {
-            const int ty = tid >> 3, tx = tid & 7;
+            const int ty = tid / G, tx = tid % G;
             bool need = false;
 #pragma unroll
             for (int bk = 0; bk < RM; ++bk) {
-                while (!need && k < p && (k >> 3) == bk) {
+                while (!need && k < p && k / G == bk) {
                     if (stamping) t_mark = __builtin_amdgcn_s_memtime();
-                    const bool mine = tx == (k & 7);
+                    const bool mine = tx == k % G;
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
-                        const int i = ty + 8 * a;
+                        const int i = ty + G * a;
                         double* dst = (mine && i >= k && i < m) ? colv + i : st.F - 1;
                         *dst = R[a][bk];
                     }
                     __syncthreads();
                     const double akk = colv[k];
                     const int q = k + 1 + tid;
-                    const double x = colv[q < m ? q : m - 1];
+                    // unclamped reads: colv has G*RM readable entries (factor_lds_bytes slack), so
+                    // each read is one base register plus an immediate offset
+                    double x = colv[q < m ? q : m - 1];
                     double lv[RM], cv[RM];
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
-                        const int i = ty + 8 * a, j = tx + 8 * a;
-                        const double vi = colv[i < m ? i : m - 1], vj = colv[j < m ? j : m - 1];
-                        lv[a] = (i > k && i < m) ? vi : 0.0;
-                        cv[a] = (j > k && j < m) ? vj : 0.0;
+                        lv[a] = colv[ty + G * a];
+                        cv[a] = colv[tx + G * a];
+                    }
+                    // keep the reads unconditional (all issued before the first wait): sunk under
+                    // the masks below they become one divergent branch + LDS wait per element
+                    asm volatile("" : "+v"(x));
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) asm volatile("" : "+v"(lv[a]), "+v"(cv[a]));
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) {
+                        const int i = ty + G * a, j = tx + G * a;
+                        lv[a] = (i > k && i < m) ? lv[a] : 0.0;
+                        cv[a] = (j > k && j < m) ? cv[a] : 0.0;
                     }
                     const double aak = fabs(akk);
                     const bool bad = !(aak > thres) || (q < m && A.u * fabs(x) > aak);
-                    need = __ballot(bad) != 0;
+                    if constexpr (W == 1) {
+                        need = __ballot(bad) != 0;
+                    } else {
+                        // every wave tests its rows; a failing wave marks the step, a second
+                        // barrier publishes the verdict (and frees colv for the next step)
+                        if (__ballot(bad) != 0 && (tid & 63) == 0) sh->failk = k;
+                        __syncthreads();
+                        need = sh->failk == k;
+                    }
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange: rank-1 update in registers
                         const double dinv = 1.0 / akk;
@@ -495,7 +526,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                 }
             }
             if (!need) break;
-            reg_store<RM>(st, m, R);
+            reg_store<G, RM>(st, m, R);
             __syncthreads();
         }
         if (stamping) t_mark = __builtin_amdgcn_s_memtime();
@@ -543,8 +574,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             const double dk = st.at(k, k);
             const double dinv = 1.0 / dk;
             if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_rest += t - t_mark; t_mark = t; }
-            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), false>(st, m, k, dinv, 0.0, 0.0);
-            else schur_update_generic<kGrid<NT>, false>(st, m, k, dinv, 0.0, 0.0);
+            // rare fallback steps of the register path use the low-register generic update, so the
+            // kernel's VGPR budget (occupancy) is set by the register-resident fast path
+            schur_update_generic<kGrid<NT>, false>(st, m, k, dinv, 0.0, 0.0);
             if (tid == 0) { piv[k] = PIV_1X1; if (dk > 0.0) npos++; else nneg++; }
             __syncthreads();
             if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; t_mark = t; }
@@ -553,8 +585,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
             const double det = a * e - b * b;
             const double idet = 1.0 / det;
-            if (MR > 0) schur_update_tile<kGrid<NT>, (MR > 0 ? MR : 1), true>(st, m, k, a * idet, b * idet, e * idet);
-            else schur_update_generic<kGrid<NT>, true>(st, m, k, a * idet, b * idet, e * idet);
+            schur_update_generic<kGrid<NT>, true>(st, m, k, a * idet, b * idet, e * idet);
             if (tid == 0) {
                 piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; n2++;
                 if (det < 0.0) { npos++; nneg++; }
@@ -564,10 +595,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             __syncthreads();
             k += 2;
         }
-        if constexpr (REG) reg_load<RM>(st, m, R);
+        if constexpr (REG) reg_load<G, RM>(st, m, R);
     }
     if constexpr (REG) {
-        reg_store<RM>(st, m, R);
+        reg_store<G, RM>(st, m, R);
         __syncthreads();
     }
     if (A.stamps && tid == 0) {
@@ -764,7 +795,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 __device__ __forceinline__ int64_t packed_even(int m) { return (((int64_t)m * (m + 1) / 2) + 1) & ~1ll; }
 
 template <int NT, int MR>
-__global__ __launch_bounds__(NT) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 3 : 1))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
     const int f = fronts[blockIdx.x];
@@ -1151,8 +1182,10 @@ hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hip
 
 size_t factor_lds_bytes(int mmax) {
     const size_t packed = (((size_t)mmax * (mmax + 1) / 2) + 1) & ~(size_t)1;
+    // + slack: the register path reads the column vector (coefB) unclamped up to 2*kThreads... entries
+    const int grid_rows = mmax <= 32 ? 32 : (mmax <= 64 ? 64 : 2 * kThreads);
     return 32 + packed * sizeof(double) + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
-           (size_t)((mmax + 15) & ~15);
+           (size_t)((mmax + 15) & ~15) + (size_t)grid_rows * sizeof(double);
 }
 
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
