@@ -11,7 +11,7 @@ if os.environ.get("LEAF"):
     g.set_option("leaf_size", int(os.environ["LEAF"]))
 g.analyze(N, r, c)
 g.factorize(v); g.inertia()
-g.set_option("stamps", 1)
+g.set_option("stamps", int(os.environ.get("MODE", "1")))
 g.factorize(v); g.inertia()
 lib = g.lib
 nf = g.stats()["n_fronts"]
@@ -26,6 +26,13 @@ loop = (st[:, 2] - st[:, 1]) * 10e-3
 wout = (st[:, 3] - st[:, 2]) * 10e-3
 cs = st[:, 4]; cu = st[:, 5]; cr = st[:, 6]; steps = np.maximum(st[:, 7], 1)
 print("fronts", nf, "levels", fl.max() + 1)
+if os.environ.get("MODE") == "2":
+    w = (st[:, 4:8] - st[:, [2, 4, 5, 6]]) * 10e-3
+    for lev in range(fl.max() + 1):
+        s = fl == lev
+        print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} | write: coef {w[s,0].mean():6.2f} L {w[s,1].mean():6.2f} "
+              f"rows {w[s,2].mean():6.2f} cb {w[s,3].mean():6.2f} tail {((st[s,3]-st[s,7])*10e-3).mean():6.2f} us")
+    sys.exit(0)
 for lev in range(fl.max() + 1):
     s = fl == lev
     print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} p {fp[s].mean():5.1f} | assemble {asm[s].mean():7.2f} us "

@@ -403,6 +403,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     A.stamps = nullptr;
+    A.stamp_mode = h->want_stamps;
     if (h->want_stamps) {
         if (h->stamps.n != (size_t)(8 * S.nf)) HIPCHK(h, h->stamps.alloc(8 * S.nf));
         HIPCHK(h, hipMemsetAsync(h->stamps.p, 0, sizeof(unsigned long long) * 8 * S.nf, s));
@@ -465,7 +466,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "dense_factor") h->aopt.dense_factor = value;
     else if (n == "timing") h->timing = value != 0.0;
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
-    else if (n == "stamps") h->want_stamps = value != 0.0;
+    else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;

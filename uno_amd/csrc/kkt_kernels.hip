@@ -202,6 +202,7 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long x, i
     unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
     return ((unsigned long long)hi << 32) | lo;
 }
+__device__ __forceinline__ double readlane_d(double x, int l) { return as_double(readlane64(as_bits(x), l)); }
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 // max over the 64 lanes of a wave (every lane must be active)
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
@@ -601,12 +602,15 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         reg_store<G, RM>(st, m, R);
         __syncthreads();
     }
+    const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
-        A.stamps[8 * f + 4] = cyc_search;
-        A.stamps[8 * f + 5] = cyc_update;
-        A.stamps[8 * f + 6] = cyc_rest;
-        A.stamps[8 * f + 7] = (unsigned long long)p;
+        if (!sub) {
+            A.stamps[8 * f + 4] = cyc_search;
+            A.stamps[8 * f + 5] = cyc_update;
+            A.stamps[8 * f + 6] = cyc_rest;
+            A.stamps[8 * f + 7] = (unsigned long long)p;
+        }
     }
     // ---- write L: packed lower trapezoid, column j rows j..m-1 ----
     // per-column coefficients first (one division per column, not per entry):
@@ -627,23 +631,42 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         coefB[j] = cbv;
     }
     __syncthreads();
+    if (sub) A.stamps[8 * f + 4] = __builtin_amdgcn_s_memrealtime();
     double* L = A.L + A.L_off[f];
     if (NT == 64 && m <= 64) {
-        // one wave, m <= 64: column j is one coalesced store, lane = row offset from the diagonal
+        // one wave, m <= 64: column j is one coalesced store, lane = row offset from the diagonal.
+        // Per-column data lives in lane j and is broadcast with readlane (scalar, uniform control).
+        const int mykind = tid < p ? (int)piv[tid] : 0;
+        const double myca = tid < p ? coefA[tid] : 0.0, mycb = tid < p ? coefB[tid] : 0.0;
         int64_t cs = 0;  // start of column j
-#pragma unroll 4
-        for (int j = 0; j < p; ++j) {
-            const int i = j + tid;
-            const int8_t kind = piv[j];
-            const int base = kind == PIV_2X2_B ? j - 1 : j;
-            const int ii = i < m ? i : m - 1;
-            const double x0 = st.at(ii, base), x1 = st.at(ii, base + (base + 1 < m ? 1 : 0));
-            double v = coefA[j] * x0;
-            if (kind >= PIV_2X2_A) v += coefB[j] * x1;
-            if (i == j) v = kind == PIV_NULL ? 0.0 : st.at(j, j);
-            else if (kind == PIV_2X2_A && i == j + 1) v = x0;  // D off-diagonal A(j+1, j)
-            if (i < m) L[cs + tid] = v;
-            cs += m - j;
+        for (int j0 = 0; j0 < p; j0 += 4) {
+            double v[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u < p ? j0 + u : p - 1;
+                const int kind = __builtin_amdgcn_readlane(mykind, j);
+                const double ca = readlane_d(myca, j), cb2 = readlane_d(mycb, j);
+                const int base = kind == PIV_2X2_B ? j - 1 : j;
+                const int i = j + tid;
+                const int ii = i < m ? i : m - 1;
+                const int rs = (ii * (ii + 1)) >> 1;
+                const double x0 = st.F[rs + base];
+                const double x1 = st.F[rs + (base + 1 <= ii ? base + 1 : base)];
+                const double dj = st.F[((j * (j + 1)) >> 1) + j];
+                double w = ca * x0;
+                if (kind >= PIV_2X2_A) w += cb2 * x1;  // uniform
+                if (i == j) w = kind == PIV_NULL ? 0.0 : dj;
+                else if (kind == PIV_2X2_A && i == j + 1) w = x0;  // D off-diagonal A(j+1, j)
+                v[u] = w;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; ++u) {
+                const int j = j0 + u;
+                if (j < p) {  // uniform
+                    if (j + tid < m) L[cs + tid] = v[u];
+                    cs += m - j;
+                }
+            }
         }
     } else {
         const int64_t total = (int64_t)p * m - (int64_t)p * (p - 1) / 2;
@@ -667,24 +690,35 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             L[t] = v;
         }
     }
+    if (sub) A.stamps[8 * f + 5] = __builtin_amdgcn_s_memrealtime();
     // ---- permuted row ids and pivot kinds ----
     for (int i = tid; i < m; i += NT) {
         A.frow[A.rows_off[f] + i] = lrow[i];
         A.fpos[A.rows_off[f] + lorig[i]] = i;  // analysis-order local row -> pivoted position
         if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
     }
+    if (sub) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
     // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
     const int cm = m - p;
     if (cm > 0) {
         double* cb = A.cb + A.cb_off[f];
         const int ctot = cm * (cm + 1) / 2;
-#pragma unroll 4
-        for (int t = tid; t < ctot; t += NT) {
-            int r, c;
-            tri_rc(t, r, c);
-            cb[t] = st.at(p + r, p + c);
+        constexpr int WB = 4;  // batch: all LDS reads, then all stores (one LDS wait per batch)
+        for (int t0 = tid; t0 < ctot; t0 += WB * NT) {
+            double v[WB];
+#pragma unroll
+            for (int u = 0; u < WB; ++u) {
+                const int t = t0 + u * NT;
+                int r, c;
+                tri_rc(t < ctot ? t : ctot - 1, r, c);
+                v[u] = st.at(p + r, p + c);
+            }
+#pragma unroll
+            for (int u = 0; u < WB; ++u)
+                if (t0 + u * NT < ctot) cb[t0 + u * NT] = v[u];
         }
     }
+    if (sub) A.stamps[8 * f + 7] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
         A.fstat[f] = (int32_t)((nstuck > 0xffff ? 0xffff : nstuck) | ((nrel > 0x7fff ? 0x7fff : nrel) << 16));
         // per-front record instead of global atomics: thousands of fronts finishing together would
@@ -849,7 +883,6 @@ __global__ void k_unscale(const double* __restrict__ w, const double* __restrict
         x[i] = scale[i] * w[i];
 }
 
-__device__ __forceinline__ double readlane_d(double x, int l) { return as_double(readlane64(as_bits(x), l)); }
 
 // wave-wide sum (all lanes active); result wave-uniform
 __device__ __forceinline__ double wave_sum(double x) {

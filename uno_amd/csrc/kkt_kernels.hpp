@@ -40,7 +40,8 @@ struct FactorArgs {
     const int32_t* fparent;     // assembly-tree parent (-1 = root)
     int32_t* delayed;           // original ids of columns that failed the threshold (counters[6] = count)
     int record_delays;
-    unsigned long long* stamps;  // diagnostics (nullptr in normal runs): per front 8 words
+    unsigned long long* stamps;
+    int stamp_mode;  // 1: phases + cycle counts, 2: write-out sub-phases in slots 4..7  // diagnostics (nullptr in normal runs): per front 8 words
     double u;
     double null_fac;
 };
