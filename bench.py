@@ -6,9 +6,14 @@ Uno's ipopt-preset layout, uno_amd/csrc/arrowband.c).  A step is one numerical L
 + one inertia query + one nrhs=1 solve, after an untimed symbolic analysis; values and right-hand
 side are already resident in HBM when the timed region starts.
 
-Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): every rank
-factors and solves its own independent KKT system (independent objects, no data-path collective,
-weak scaling); value = all ranks' factor+solves / max-over-ranks time.
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N), default
+--mode dist: ONE arrowband KKT of dimension N x 1e6 (weak scaling: 1e6 rows per
+GPU) is factored and solved across the N GPUs -- independent elimination subtrees per rank, the
+subtree roots' contribution blocks / update vectors sent to rank 0 over RCCL (xGMI) for the top of
+the assembly tree, the top rows of the solution broadcast back, inertia all-reduced, the solution
+gathered on rank 0.  value = (N x 1e6 / 1e6) factor+solves per second, i.e. n=1e6-equivalent
+factor+solves/s of the whole job (factor flops, L bytes and solve bytes of the arrowband family all
+grow linearly in n).  --mode replicas: an independent C3 system per GPU (no data-path collective).
 
 Prints ONE JSON line on rank 0 (contract in the task statement), with `roofline` for the dominant
 kernel class (HIP events on the solver's stream, second timed pass) and `cpu_baseline` from the CPU
@@ -34,7 +39,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000, help="KKT dimension (C3 = 1e6)")
+    ap.add_argument("--n", type=int, default=1_000_000, help="KKT dimension per GPU (C3 = 1e6)")
+    ap.add_argument("--mode", choices=["dist", "replicas"], default="dist",
+                    help="N>1: one system partitioned over the GPUs (dist) or one system per GPU (replicas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-n", type=int, default=1_000_000)
     ap.add_argument("--profile-only", action="store_true", help="skip event pass and CPU baseline")
@@ -58,9 +65,19 @@ def main():
 
     import uno_amd
     uno_amd.load_library()
-    seed = uno_amd.SEEDS["C3"] + rank  # independent system per rank
-    n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(args.n, seed)
+    dist_mode = world > 1 and args.mode == "dist"
+    if dist_mode:  # one system of dimension world * n, the same on every rank
+        seed = uno_amd.SEEDS["C3"]
+        n_total = args.n * world
+    else:          # independent system per rank
+        seed = uno_amd.SEEDS["C3"] + rank
+        n_total = args.n
+    n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(n_total, seed)
     kkt = uno_amd.HipKKT(local)
+    if dist_mode:
+        from uno_amd.replicas import share_bytes
+        uid = share_bytes(uno_amd.rccl_unique_id() if rank == 0 else None, world)
+        kkt.attach_rccl(uid, rank, world)
     if args.leaf:
         kkt.set_option("leaf_size", args.leaf)
     if args.block:
@@ -83,12 +100,16 @@ def main():
     from uno_amd.replicas import aggregate, timed_steps
     elapsed, inertia = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, dev)
 
-    # parity sanity on the measured system: relative residual of the last solve
-    x = x_d.cpu().numpy()
-    res = np.abs(uno_amd.coo_symv(n, rows, cols, vals, x) - rhs).max()
-    absk = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max()
-    rel_res = float(res / (absk * np.abs(x).max() + np.abs(rhs).max()))
+    # parity sanity on the measured system: relative residual of the last solve (rank 0 holds the
+    # complete solution in dist mode)
+    rel_res = None
+    if rank == 0 or not dist_mode:
+        x = x_d.cpu().numpy()
+        res = np.abs(uno_amd.coo_symv(n, rows, cols, vals, x) - rhs).max()
+        absk = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max()
+        rel_res = float(res / (absk * np.abs(x).max() + np.abs(rhs).max()))
     st = kkt.stats()
+    dinfo = kkt.dist_info() if dist_mode else None
 
     # second timed pass with per-kernel HIP events on the solver stream (roofline)
     ktimes = {}
@@ -107,13 +128,18 @@ def main():
             dist.destroy_process_group()
         return
 
+    # whole-job throughput in n=1e6-equivalent factor+solves (dist: one system of world * n rows)
     value, ms_per_step = aggregate(args.steps, world, elapsed)
+    if dist_mode:
+        value = args.steps * (n_total / 1_000_000) / elapsed
 
-    # ---- roofline of the dominant kernel class ----
+    # ---- roofline of the dominant kernel class (rank 0's kernels) ----
     K = args.steps
     n2 = st["pivots_2x2"]
     bytes_solve = 8.0 * (2 * st["nnz_L"] + n + n2) + 24.0 * n      # SURVEY 8(d) B_solve, per solve
     flops_fac = st["flops"]                                         # per factorization
+    if dist_mode:  # rank 0's share: its subtrees + the top of the tree
+        flops_fac = dinfo["my_flops"] + dinfo["top_flops"]
     bytes_fac = 8.0 * (st["nnz_unique"] + st["nnz_L"] + n)          # B_min per factorization
     roof = None
     if ktimes:
@@ -145,7 +171,7 @@ def main():
 
     # ---- CPU baseline: the oracle (MUMPS restatement) on the host, one core ----
     cpu = None
-    if not args.no_cpu_baseline and not args.profile_only:
+    if not args.no_cpu_baseline and not args.profile_only and world == 1:
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         from oracle_ffi import OracleKKT
         cn, _, _, cr, cc, cv, cb = uno_amd.arrowband(args.cpu_baseline_n, uno_amd.SEEDS["C3"])
@@ -175,7 +201,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (arrowband KKT generator, SURVEY 8(d), seed 0x5EED0003+rank)",
+        "data": ("synthetic (arrowband KKT generator, SURVEY 8(d), seed 0x5EED0003, one system over all ranks)"
+                 if dist_mode else "synthetic (arrowband KKT generator, SURVEY 8(d), seed 0x5EED0003+rank)"),
         "config": {"workload": "C3 arrowband KKT, ipopt-preset COO layout, factor+inertia+solve",
                    "n": n, "nv": nv, "m": m, "nnz": int(len(vals)), "nnz_unique": st["nnz_unique"],
                    "nnz_L": st["nnz_L"], "fronts": st["n_fronts"], "levels": st["n_levels"],
@@ -183,7 +210,10 @@ def main():
                    "analysis_s": round(t_analysis, 3), "inertia": list(inertia),
                    "pivots_2x2": st["pivots_2x2"], "pivots_relaxed": st["pivots_relaxed"],
                    "fronts_merged": st["fronts_merged"], "rel_residual": rel_res,
-                   "parallelism": f"replicas x{world} (independent KKT per GPU)"},
+                   "parallelism": (f"subtree-partitioned x{world} (RCCL root exchange to rank 0)" if dist_mode
+                                   else f"replicas x{world} (independent KKT per GPU)"),
+                   "value_unit_note": "n=1e6-equivalent factor+solves per second of the whole job",
+                   "dist": dinfo},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

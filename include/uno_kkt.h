@@ -105,6 +105,36 @@ void* uno_kkt_stream(uno_kkt_t handle);
 /* Human-readable description of the last error on this handle ("" if none). */
 const char* uno_kkt_last_error(uno_kkt_t handle);
 
+/* ---- Multi-GPU: one factorization partitioned over the GPUs of a node ----
+ * The assembly tree is cut into independent subtrees, one set per rank, factored without any
+ * communication; the subtree roots' contribution blocks go to rank 0 (RCCL point-to-point over xGMI),
+ * which factors the top of the tree.  Inertia counters are all-reduced, so every rank returns the
+ * inertia of the whole matrix.  The solve hands the subtree roots' update vectors to rank 0 and
+ * broadcasts the top rows of the solution back; with option "gather_solution" (default 1) rank 0
+ * returns the complete x (MUMPS ICNTL(21) = 0), other ranks their own rows.  Every rank calls the same
+ * sequence (analyze / factorize / inertia / solve) with the same pattern, values and rhs.
+ * The reference has no multi-process path (MUMPS par = 1, MUMPSSolver.cpp:17); this is an extension.
+ * Attach before uno_kkt_analyze. */
+int uno_kkt_comm_unique_id(unsigned char id[128]);                                     /* rank 0, shared out of band */
+int uno_kkt_attach_rccl(uno_kkt_t handle, const unsigned char id[128], int rank, int world);
+/* In-process group (several handles in one process, one host thread each; e.g. several ranks on one GPU). */
+typedef struct uno_kkt_group* uno_kkt_group_t;
+int uno_kkt_group_create(uno_kkt_group_t* group, int world);
+void uno_kkt_group_destroy(uno_kkt_group_t group);
+int uno_kkt_attach_local(uno_kkt_t handle, uno_kkt_group_t group, int rank);
+
+typedef struct {
+    int64_t rank, world;
+    int64_t subtrees;      /* independent subtrees of the partition */
+    int64_t top_fronts;    /* fronts above the cut (factored by rank 0) */
+    int64_t my_fronts;     /* fronts in this rank's subtrees */
+    int64_t own_rows;      /* rows eliminated in this rank's subtrees */
+    int64_t top_rows;      /* rows eliminated in top fronts */
+    double my_flops, top_flops;
+    double est_imbalance;  /* max rank work / mean rank work (analysis estimate) */
+} uno_kkt_dist_info_t;
+int uno_kkt_dist_info(uno_kkt_t handle, uno_kkt_dist_info_t* info);
+
 /* Library version string. */
 const char* uno_kkt_version(void);
 

@@ -9,6 +9,11 @@
 #ifdef __cplusplus
 extern "C" {
 #endif
+/* Host-only symbolic analysis + subtree partition over `world` ranks (no device): per front its owner
+ * (rank, or -1 = top front factored by rank 0) and assembly-tree parent.  Returns the number of fronts,
+ * -nf if cap is too small, -1 on a bad pattern. */
+int64_t uno_kkt_debug_partition(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int world,
+                                int32_t* owner, int32_t* parent, int64_t cap, int64_t* n_subtrees);
 int64_t uno_kkt_debug_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap, int32_t* front_order,
                              int32_t* front_pivots, int32_t* front_level);
 #ifdef __cplusplus

@@ -5,4 +5,5 @@ sources in uno_amd/csrc; uno_amd.kkt is its ctypes binding plus Python mirrors o
 surface used by the tests and bench.py.
 """
 from .kkt import (HipKKT, HipLDLSolver, KKTError, SparseSymmetricMatrix, UnstableRegularization,  # noqa: F401
-                  arrowband, coo_symv, load_library, regularize_augmented_matrix, SEEDS)
+                  arrowband, coo_symv, load_library, regularize_augmented_matrix, SEEDS,
+                  LocalGroup, rccl_unique_id, debug_partition)

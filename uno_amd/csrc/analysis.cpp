@@ -540,4 +540,99 @@ int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge
     return merged;
 }
 
+// Greedy top-down cut: repeatedly move the heaviest candidate subtree's root into the top set (its
+// children become candidates), pack the candidates onto the ranks longest-first, and keep the cut
+// with the smallest estimated critical path = makespan of the packed subtrees + serial top work.
+void partition_tree(const Symbolic& S, int world, Partition& out) {
+    const int32_t nf = (int32_t)S.nf;
+    out = Partition();
+    out.world = world;
+    out.owner.assign(nf, 0);
+    if (world <= 1 || nf == 0) return;
+    // per-front cost estimate: factor flops + assembly + a per-pivot-step latency term
+    std::vector<double> work(nf), sub(nf, 0.0);
+    std::vector<std::vector<int32_t>> kids(nf);
+    for (int32_t f = 0; f < nf; ++f) {
+        const double m = S.f_m[f], p = S.f_p[f];
+        double fl = 0.0;
+        for (int k = 0; k < (int)p; ++k) {
+            const double r = m - k - 1;
+            fl += r + r * (r + 1.0);
+        }
+        work[f] = fl + m * m + 2000.0 * p;
+    }
+    for (int32_t f = 0; f < nf; ++f) {  // children have smaller ids
+        sub[f] += work[f];
+        if (S.f_parent[f] >= 0) {
+            sub[S.f_parent[f]] += sub[f];
+            kids[S.f_parent[f]].push_back(f);
+        }
+    }
+    std::vector<int32_t> cand;
+    double total = 0.0;
+    for (int32_t f = 0; f < nf; ++f)
+        if (S.f_parent[f] < 0) { cand.push_back(f); total += sub[f]; }
+    out.total_work = total;
+    auto pack = [&](const std::vector<int32_t>& c, std::vector<int32_t>* assign) {
+        std::vector<int32_t> order(c.begin(), c.end());
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return sub[a] > sub[b]; });
+        std::vector<double> load(world, 0.0);
+        if (assign) assign->assign(nf, -1);
+        for (int32_t r : order) {
+            int best = 0;
+            for (int q = 1; q < world; ++q)
+                if (load[q] < load[best]) best = q;
+            load[best] += sub[r];
+            if (assign) (*assign)[r] = best;
+        }
+        return *std::max_element(load.begin(), load.end());
+    };
+    std::vector<char> top(nf, 0);
+    double top_work = 0.0;
+    double best_cost = pack(cand, nullptr);
+    std::vector<char> best_top = top;
+    std::vector<int32_t> best_cand = cand;
+    double best_top_work = 0.0;
+    const int max_cuts = 64 * world;
+    int since_best = 0;
+    for (int cut = 0; cut < max_cuts && since_best < 8 * world; ++cut) {
+        // split the heaviest candidate that has children
+        int pick = -1;
+        for (size_t q = 0; q < cand.size(); ++q)
+            if (!kids[cand[q]].empty() && (pick < 0 || sub[cand[q]] > sub[cand[pick]])) pick = (int)q;
+        if (pick < 0) break;
+        const int32_t f = cand[pick];
+        cand.erase(cand.begin() + pick);
+        for (int32_t c : kids[f]) cand.push_back(c);
+        top[f] = 1;
+        top_work += work[f];
+        const double cost = pack(cand, nullptr) + top_work;
+        if (cost < best_cost * (1.0 - 1e-9)) {
+            best_cost = cost;
+            best_top = top;
+            best_cand = cand;
+            best_top_work = top_work;
+            since_best = 0;
+        } else {
+            ++since_best;
+        }
+    }
+    std::vector<int32_t> root_owner;
+    out.max_rank_work = pack(best_cand, &root_owner);
+    out.top_work = best_top_work;
+    out.n_subtrees = (int64_t)best_cand.size();
+    // owner of every front: top fronts -1, others inherit the rank of their subtree root
+    for (int32_t f = nf - 1; f >= 0; --f) {
+        if (best_top[f]) { out.owner[f] = -1; out.n_top++; continue; }
+        if (root_owner[f] >= 0) { out.owner[f] = root_owner[f]; continue; }
+        out.owner[f] = out.owner[S.f_parent[f]];  // parent id is larger: already set
+    }
+    for (int32_t r : best_cand) {
+        if (S.f_parent[r] >= 0) {
+            out.send_roots.push_back(r);
+            out.root_rank.push_back(root_owner[r]);
+        }
+    }
+}
+
 }  // namespace ukkt

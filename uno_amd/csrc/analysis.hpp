@@ -82,6 +82,20 @@ int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge
 // is moved into its parent's block (eliminated just before the parent's own columns).
 int64_t delay_columns(Pattern& P, const Symbolic& S, const std::vector<int32_t>& delayed_vars);
 
+// Subtree partition of the assembly tree over `world` ranks: the top of the tree is
+// cut until the remaining subtrees can be packed onto the ranks with a small makespan; every subtree
+// is factored by one rank without communication, the cut-off top fronts by rank 0 after the subtree
+// roots' contribution blocks arrive.  Deterministic: every rank computes the same partition.
+struct Partition {
+    int world = 1;
+    std::vector<int32_t> owner;       // per front: rank, or -1 for a top front (rank 0, after the exchange)
+    std::vector<int32_t> send_roots;  // subtree roots whose parent is a top front
+    std::vector<int32_t> root_rank;   // rank owning send_roots[k]
+    int64_t n_subtrees = 0, n_top = 0;
+    double total_work = 0.0, top_work = 0.0, max_rank_work = 0.0;
+};
+void partition_tree(const Symbolic& S, int world, Partition& out);
+
 inline std::string analyze(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col,
                            const AnalysisOptions& opt, Pattern& P, Symbolic& S) {
     std::string e = order_pattern(n, nnz, row, col, opt, P);

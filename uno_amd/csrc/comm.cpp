@@ -1,0 +1,200 @@
+// comm.cpp -- RCCL and in-process transports (see comm.hpp).
+#include "comm.hpp"
+
+#include <rccl/rccl.h>
+
+#include <condition_variable>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <vector>
+
+namespace ukkt {
+
+// ------------------------------------------------------------------------------------------------
+// in-process group
+// ------------------------------------------------------------------------------------------------
+struct LocalGroup {
+    int world;
+    std::mutex mu;
+    std::condition_variable cv;
+    struct Msg {
+        const void* buf;
+        size_t bytes;
+        hipEvent_t ev;
+    };
+    std::vector<std::deque<Msg>> box;  // src * world + dst
+    int arrived = 0;
+    uint64_t gen = 0;
+    std::vector<std::vector<uint64_t>> contrib;
+    std::vector<uint64_t> result;
+    const void* bptr = nullptr;
+    hipEvent_t bev = nullptr;
+    explicit LocalGroup(int w) : world(w), box((size_t)w * w), contrib(w) {}
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t g = gen;
+        if (++arrived == world) {
+            arrived = 0;
+            ++gen;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return gen != g; });
+        }
+    }
+};
+
+LocalGroup* local_group_create(int world) { return world > 0 ? new LocalGroup(world) : nullptr; }
+void local_group_destroy(LocalGroup* g) { delete g; }
+
+namespace {
+
+class LocalTransport final : public Transport {
+public:
+    LocalTransport(LocalGroup* g, int r) : g_(g), r_(r) {}
+    int rank() const override { return r_; }
+    int size() const override { return g_->world; }
+    std::string describe() const override { return "local(in-process, " + std::to_string(g_->world) + " ranks)"; }
+
+    hipError_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+        hipEvent_t ev;
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) return e;
+        if ((e = hipEventRecord(ev, s)) != hipSuccess) return e;
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            g_->box[(size_t)r_ * g_->world + peer].push_back({buf, bytes, ev});
+        }
+        g_->cv.notify_all();
+        return hipSuccess;
+    }
+    hipError_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+        LocalGroup::Msg m;
+        {
+            std::unique_lock<std::mutex> lk(g_->mu);
+            auto& q = g_->box[(size_t)peer * g_->world + r_];
+            g_->cv.wait(lk, [&] { return !q.empty(); });
+            m = q.front();
+            q.pop_front();
+        }
+        if (m.bytes != bytes) return hipErrorInvalidValue;
+        hipError_t e = hipStreamWaitEvent(s, m.ev, 0);
+        if (e == hipSuccess && bytes) e = hipMemcpyAsync(buf, m.buf, bytes, hipMemcpyDefault, s);
+        hipEventDestroy(m.ev);
+        return e;
+    }
+    hipError_t allreduce(void* buf, size_t count, RedOp op, hipStream_t s) override {
+        std::vector<uint64_t> mine(count);
+        hipError_t e = hipStreamSynchronize(s);
+        if (e == hipSuccess && count) e = hipMemcpy(mine.data(), buf, count * 8, hipMemcpyDeviceToHost);
+        {
+            std::lock_guard<std::mutex> lk(g_->mu);
+            g_->contrib[r_] = std::move(mine);
+        }
+        g_->barrier();
+        std::vector<uint64_t> out(g_->contrib[0]);
+        for (int q = 1; q < g_->world; ++q) {  // rank order: deterministic
+            const auto& c = g_->contrib[q];
+            for (size_t i = 0; i < count && i < c.size(); ++i) {
+                switch (op) {
+                    case RedOp::SumU64: out[i] += c[i]; break;
+                    case RedOp::MaxU64: out[i] = out[i] > c[i] ? out[i] : c[i]; break;
+                    case RedOp::MaxF64:
+                    case RedOp::SumF64: {
+                        double a, b;
+                        memcpy(&a, &out[i], 8);
+                        memcpy(&b, &c[i], 8);
+                        a = op == RedOp::SumF64 ? a + b : (a > b ? a : b);
+                        memcpy(&out[i], &a, 8);
+                    } break;
+                }
+            }
+        }
+        g_->barrier();  // every rank has read every contribution
+        if (e == hipSuccess && count) e = hipMemcpy(buf, out.data(), count * 8, hipMemcpyHostToDevice);
+        return e;
+    }
+    hipError_t broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+        hipError_t e = hipSuccess;
+        hipEvent_t ev = nullptr;
+        if (r_ == root) {
+            e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+            if (e == hipSuccess) e = hipEventRecord(ev, s);
+            std::lock_guard<std::mutex> lk(g_->mu);
+            g_->bptr = buf;
+            g_->bev = ev;
+        }
+        g_->barrier();
+        if (r_ != root && bytes) {
+            e = hipStreamWaitEvent(s, g_->bev, 0);
+            if (e == hipSuccess) e = hipMemcpyAsync(buf, g_->bptr, bytes, hipMemcpyDefault, s);
+        }
+        g_->barrier();  // every copy is enqueued behind the event
+        if (ev) hipEventDestroy(ev);
+        return e;
+    }
+
+private:
+    LocalGroup* g_;
+    int r_;
+};
+
+// ------------------------------------------------------------------------------------------------
+// RCCL
+// ------------------------------------------------------------------------------------------------
+class RcclTransport final : public Transport {
+public:
+    RcclTransport(ncclComm_t c, int r, int w) : c_(c), r_(r), w_(w) {}
+    ~RcclTransport() override { ncclCommDestroy(c_); }
+    int rank() const override { return r_; }
+    int size() const override { return w_; }
+    std::string describe() const override { return "rccl(" + std::to_string(w_) + " ranks)"; }
+    hipError_t group_begin() override { return st(ncclGroupStart()); }
+    hipError_t group_end() override { return st(ncclGroupEnd()); }
+    hipError_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+        return st(ncclSend(buf, bytes, ncclUint8, peer, c_, s));
+    }
+    hipError_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+        return st(ncclRecv(buf, bytes, ncclUint8, peer, c_, s));
+    }
+    hipError_t allreduce(void* buf, size_t count, RedOp op, hipStream_t s) override {
+        ncclDataType_t t = (op == RedOp::SumU64 || op == RedOp::MaxU64) ? ncclUint64 : ncclFloat64;
+        ncclRedOp_t o = (op == RedOp::SumU64 || op == RedOp::SumF64) ? ncclSum : ncclMax;
+        return st(ncclAllReduce(buf, buf, count, t, o, c_, s));
+    }
+    hipError_t broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+        return st(ncclBroadcast(buf, buf, bytes, ncclUint8, root, c_, s));
+    }
+
+private:
+    static hipError_t st(ncclResult_t r) { return r == ncclSuccess ? hipSuccess : hipErrorLaunchFailure; }
+    ncclComm_t c_;
+    int r_, w_;
+};
+
+}  // namespace
+
+Transport* make_local_transport(LocalGroup* g, int rank) {
+    if (!g || rank < 0 || rank >= g->world) return nullptr;
+    return new LocalTransport(g, rank);
+}
+
+int rccl_unique_id(unsigned char out[128]) {
+    static_assert(sizeof(ncclUniqueId) == 128, "NCCL_UNIQUE_ID_BYTES");
+    ncclUniqueId id;
+    if (ncclGetUniqueId(&id) != ncclSuccess) return -1;
+    memcpy(out, &id, 128);
+    return 0;
+}
+
+Transport* make_rccl_transport(const unsigned char id[128], int rank, int world, int device, std::string& err) {
+    ncclUniqueId uid;
+    memcpy(&uid, id, 128);
+    if (hipSetDevice(device) != hipSuccess) { err = "hipSetDevice failed"; return nullptr; }
+    ncclComm_t c;
+    ncclResult_t r = ncclCommInitRank(&c, world, uid, rank);
+    if (r != ncclSuccess) { err = std::string("ncclCommInitRank: ") + ncclGetErrorString(r); return nullptr; }
+    return new RcclTransport(c, rank, world);
+}
+
+}  // namespace ukkt

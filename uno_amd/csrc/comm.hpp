@@ -1,0 +1,52 @@
+// comm.hpp -- inter-GPU transport of the distributed (subtree-partitioned) factorization.
+//
+// independent elimination subtrees are factored on different GPUs; the only data
+// exchanges are the contribution blocks (factor) and update vectors (forward solve) of the subtree
+// roots, sent to the rank that owns the top of the assembly tree, the broadcast of the top rows of
+// the solution (backward solve), and small reductions (equilibration of the separator rows, the
+// null-pivot norm, inertia counters).  Two implementations:
+//   RcclTransport  -- one process per GPU, RCCL point-to-point + collectives over xGMI;
+//   LocalTransport -- several handles in one process (threads), device-to-device copies; used to run
+//                     and test the distributed algorithm on a single GPU.
+// The reference has no multi-process path (MUMPS par=1, MUMPSSolver.cpp:17); this is new.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+#include <string>
+
+namespace ukkt {
+
+enum class RedOp { SumU64, MaxU64, MaxF64, SumF64 };
+
+class Transport {
+public:
+    virtual ~Transport() = default;
+    virtual int rank() const = 0;
+    virtual int size() const = 0;
+    // point-to-point, stream-ordered; a batch of sends/recvs is bracketed by group_begin/group_end
+    virtual hipError_t group_begin() { return hipSuccess; }
+    virtual hipError_t group_end() { return hipSuccess; }
+    virtual hipError_t send(const void* buf, size_t bytes, int peer, hipStream_t s) = 0;
+    virtual hipError_t recv(void* buf, size_t bytes, int peer, hipStream_t s) = 0;
+    // in-place all-reduce of `count` elements of a device buffer
+    virtual hipError_t allreduce(void* buf, size_t count, RedOp op, hipStream_t s) = 0;
+    // in-place broadcast of a device buffer from `root`
+    virtual hipError_t broadcast(void* buf, size_t bytes, int root, hipStream_t s) = 0;
+    virtual std::string describe() const = 0;
+};
+
+// Local (in-process) group: create once with the world size, attach one handle per rank; every rank
+// must be driven by its own host thread (collectives block until all ranks have arrived).
+struct LocalGroup;
+LocalGroup* local_group_create(int world);
+void local_group_destroy(LocalGroup* g);
+Transport* make_local_transport(LocalGroup* g, int rank);
+
+// RCCL: unique id from rank 0 (NCCL_UNIQUE_ID_BYTES = 128), then every rank attaches with it.
+int rccl_unique_id(unsigned char out[128]);
+Transport* make_rccl_transport(const unsigned char id[128], int rank, int world, int device, std::string& err);
+
+}  // namespace ukkt

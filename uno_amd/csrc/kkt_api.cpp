@@ -16,6 +16,7 @@
 #include "../../include/uno_kkt.h"
 #include "../../include/uno_kkt_debug.h"
 #include "analysis.hpp"
+#include "comm.hpp"
 #include "kkt_kernels.hpp"
 
 using namespace ukkt;
@@ -60,6 +61,35 @@ struct SolveLaunch {
     bool wave;
 };
 
+// launch plan of a set of fronts: factor launches index fac_fronts, solve launches sol_fronts
+struct Plan {
+    DBuf<int32_t> fac_fronts, sol_fronts;
+    std::vector<Launch> fac;
+    std::vector<SolveLaunch> sol;  // ordered by level
+};
+
+// per-rank data of a distributed (subtree-partitioned) factorization, SURVEY.md 8(e)
+struct DistState {
+    Partition part;
+    std::vector<std::pair<int64_t, int64_t>> pack_ranges;  // packed slot ranges of the rank's fronts
+    DBuf<int32_t> own_new, own_orig, own_long;             // rows eliminated in the rank's subtrees
+    int64_t n_own = 0;
+    int32_t n_own_long = 0;
+    int64_t max_own_long = 0;
+    DBuf<int32_t> top_orig;                                // rows eliminated in top fronts
+    int64_t n_top_rows = 0;
+    DBuf<int32_t> chunk_row, pslot, ppartner;              // partial scans of the top rows
+    DBuf<int64_t> chunk_begin;
+    int64_t nchunks = 0;
+    DBuf<double> outT, tbuf, xbuf;
+    DBuf<unsigned long long> tmp;
+    std::vector<int64_t> own_count;                        // per rank (rank 0: gather of the solution)
+    DBuf<int32_t> all_own_orig;                            // rank 0: every rank's own rows, by rank
+    std::vector<int64_t> all_own_off;
+    double my_flops = 0.0, top_flops = 0.0;
+    int64_t my_fronts = 0;
+};
+
 }  // namespace
 
 struct uno_kkt {
@@ -78,7 +108,7 @@ struct uno_kkt {
     const double* values_ptr = nullptr;  // device values used by the last factorization
     // device arrays
     DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, rmax, bvec;
-    DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, level_fronts, fstat;
+    DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, fstat;
     DBuf<uint32_t> ent_lpos;
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
     DBuf<int32_t> ch_cm;
@@ -89,9 +119,12 @@ struct uno_kkt {
     int32_t n_long = 0;
     int64_t max_long = 0;
     unsigned long long* h_counters = nullptr;
-    std::vector<Launch> fac_launches;
-    std::vector<SolveLaunch> sol_launches;  // ordered by level
-    DBuf<int32_t> solve_fronts;
+    Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
+    // distributed factorization (null comm: one GPU)
+    ukkt::Transport* comm = nullptr;
+    int rank = 0, world = 1;
+    int gather_solution = 1;
+    DistState dist;
     uno_kkt_stats_t st{};
     std::string err;
     // timing
@@ -164,6 +197,250 @@ void flush_timing(uno_kkt_t h) {
 int upload_structure(uno_kkt_t h);
 int enqueue_factorization(uno_kkt_t h);
 
+// Launch plan of the fronts selected by `take`: per level, fronts sorted by order (descending) cut
+// into size classes -- factor: one kernel instance per LDS class; solve: one-wave kernels grouped by
+// the LDS their packed panel needs, larger fronts in the 256-thread kernels.
+template <class Pred>
+hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
+    const Symbolic& S = h->S;
+    P.fac.clear();
+    P.sol.clear();
+    std::vector<int32_t> ffr, sfr;
+    ffr.reserve(S.nf);
+    sfr.reserve(S.nf);
+    for (int l = 0; l < S.nlevels; ++l) {
+        std::vector<int32_t> lv;
+        for (int q = S.level_off[l]; q < S.level_off[l + 1]; ++q)
+            if (take(S.level_fronts[q])) lv.push_back(S.level_fronts[q]);  // keeps the m-descending order
+        if (lv.empty()) continue;
+        {
+            std::vector<std::pair<int, int32_t>> wv;  // (LDS doubles, front)
+            std::vector<int32_t> big;
+            for (int32_t f : lv) {
+                const int m = S.f_m[f], p = S.f_p[f];
+                if (p <= 64 && m <= kMaxLdsFront) {
+                    const int sz = p * m - p * (p - 1) / 2;
+                    wv.push_back({((sz + 1) & ~1) + m, f});
+                } else {
+                    big.push_back(f);
+                }
+            }
+            std::sort(wv.begin(), wv.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
+            size_t q = 0;
+            while (q < wv.size()) {
+                int cap = 256;
+                while (cap < wv[q].first) cap *= 2;
+                size_t r = q;
+                while (r < wv.size() && (wv[r].first > cap / 2 || cap == 256)) ++r;
+                SolveLaunch sl{l, (int)sfr.size(), (int)(r - q), wv[q].first, 0, 0, true};
+                for (size_t t = q; t < r; ++t) sfr.push_back(wv[t].second);
+                P.sol.push_back(sl);
+                q = r;
+            }
+            if (!big.empty()) {
+                SolveLaunch sl{l, (int)sfr.size(), (int)big.size(), 0, 0, 0, false};
+                for (int32_t f : big) {
+                    sfr.push_back(f);
+                    sl.mmax = std::max(sl.mmax, S.f_m[f]);
+                    sl.pmax = std::max(sl.pmax, S.f_p[f]);
+                }
+                P.sol.push_back(sl);
+            }
+        }
+        const int base = (int)ffr.size();
+        ffr.insert(ffr.end(), lv.begin(), lv.end());
+        const int e = (int)lv.size();
+        int q = 0;
+        while (q < e) {
+            int m0 = S.f_m[lv[q]];
+            bool global = m0 > kMaxLdsFront;
+            int cap = global ? 1 << 30 : (m0 > 64 ? kMaxLdsFront : (m0 > 32 ? 64 : 32));
+            int floor_ = global ? kMaxLdsFront : (cap == kMaxLdsFront ? 64 : (cap == 64 ? 32 : 0));
+            int r = q;
+            while (r < e && S.f_m[lv[r]] > floor_ && S.f_m[lv[r]] <= cap) ++r;
+            P.fac.push_back({base + q, r - q, m0, global});
+            q = r;
+        }
+    }
+    hipError_t e = P.fac_fronts.upload(ffr, h->stream);
+    if (e == hipSuccess) e = P.sol_fronts.upload(sfr, h->stream);
+    return e;
+}
+
+// Rank-local layout of a distributed factorization: subtree partition (identical on every rank),
+// the rank's packed slot ranges, its own rows (complete row scans) and the partial scans of the top
+// rows, whose per-rank partials are all-reduced.  See DESIGN.md section 6.
+int setup_distribution(uno_kkt_t h) {
+    const Symbolic& S = h->S;
+    DistState& D = h->dist;
+    hipStream_t s = h->stream;
+    partition_tree(S, h->world, D.part);
+    const Partition& Pt = D.part;
+    auto mine = [&](int32_t f) { return Pt.owner[f] == h->rank || (h->rank == 0 && Pt.owner[f] < 0); };
+    // packed slot ranges of every front this rank factors (consecutive fronts merged)
+    D.pack_ranges.clear();
+    D.my_flops = D.top_flops = 0.0;
+    D.my_fronts = 0;
+    for (int32_t f = 0; f < S.nf; ++f) {
+        double fl = 0.0;
+        for (int k = 0; k < S.f_p[f]; ++k) {
+            const double r = S.f_m[f] - k - 1;
+            fl += r + r * (r + 1.0);
+        }
+        if (Pt.owner[f] < 0) D.top_flops += fl;
+        else if (Pt.owner[f] == h->rank) { D.my_flops += fl; D.my_fronts++; }
+        if (!mine(f)) continue;
+        const int64_t b = S.f_ent_off[f], e = S.f_ent_off[f + 1];
+        if (b == e) continue;
+        if (!D.pack_ranges.empty() && D.pack_ranges.back().second == b) D.pack_ranges.back().second = e;
+        else D.pack_ranges.push_back({b, e});
+    }
+    // own rows (fully-summed columns of the rank's subtree fronts) and top rows
+    std::vector<int32_t> own_new, own_orig, own_long, top_orig, top_new;
+    std::vector<std::vector<int32_t>> per_rank(h->world);
+    for (int32_t f = 0; f < S.nf; ++f) {
+        const int64_t o = S.f_rows_off[f];
+        for (int k = 0; k < S.f_p[f]; ++k) {
+            const int32_t v = S.rows[o + k];
+            if (Pt.owner[f] < 0) { top_orig.push_back(v); top_new.push_back(S.iperm[v]); }
+            else per_rank[Pt.owner[f]].push_back(v);
+        }
+    }
+    own_orig = per_rank[h->rank];
+    for (int32_t v : own_orig) own_new.push_back(S.iperm[v]);
+    D.max_own_long = 0;
+    for (int32_t i : own_new) {
+        const int64_t len = (S.cptr[i + 1] - S.cptr[i]) + (S.rptr[i + 1] - S.rptr[i]);
+        if (len > kLongRow) { own_long.push_back(i); D.max_own_long = std::max(D.max_own_long, len); }
+    }
+    D.n_own = (int64_t)own_new.size();
+    D.n_own_long = (int32_t)own_long.size();
+    D.n_top_rows = (int64_t)top_orig.size();
+    HIPCHK(h, D.own_new.upload(own_new, s));
+    HIPCHK(h, D.own_orig.upload(own_orig, s));
+    HIPCHK(h, D.own_long.upload(own_long, s));
+    HIPCHK(h, D.top_orig.upload(top_orig, s));
+    // partial scans of the top rows: this rank's slots of each top row, in chunks
+    std::vector<int32_t> crow, pslot, ppart;
+    std::vector<int64_t> cbeg;
+    auto slot_front = [&](int64_t q) {
+        return (int32_t)(std::upper_bound(S.f_ent_off.begin(), S.f_ent_off.end(), q) - S.f_ent_off.begin() - 1);
+    };
+    for (int64_t t = 0; t < D.n_top_rows; ++t) {
+        const int32_t i = top_new[t], o = top_orig[t];
+        const size_t start = pslot.size();
+        if (h->rank == 0)  // column part: slots of the top front eliminating i
+            for (int32_t q = S.cptr[i]; q < S.cptr[i + 1]; ++q) { pslot.push_back(q); ppart.push_back(S.ent_r[q]); }
+        for (int32_t t2 = S.rptr[i]; t2 < S.rptr[i + 1]; ++t2) {
+            const int32_t q = S.rslot[t2];
+            if (mine(slot_front(q))) { pslot.push_back(q); ppart.push_back(S.ent_c[q] == o ? S.ent_r[q] : S.ent_c[q]); }
+        }
+        for (size_t b = start; b < pslot.size(); b += kLongChunk) { crow.push_back((int32_t)t); cbeg.push_back((int64_t)b); }
+    }
+    cbeg.push_back((int64_t)pslot.size());
+    D.nchunks = (int64_t)crow.size();
+    HIPCHK(h, D.chunk_row.upload(crow, s));
+    HIPCHK(h, D.chunk_begin.upload(cbeg, s));
+    HIPCHK(h, D.pslot.upload(pslot, s));
+    HIPCHK(h, D.ppartner.upload(ppart, s));
+    HIPCHK(h, D.outT.alloc(std::max<int64_t>(D.n_top_rows, 1)));
+    HIPCHK(h, D.tbuf.alloc(std::max<int64_t>(D.n_top_rows, 1)));
+    // gather of the solution on rank 0
+    D.own_count.assign(h->world, 0);
+    for (int q = 0; q < h->world; ++q) D.own_count[q] = (int64_t)per_rank[q].size();
+    if (h->rank == 0) {
+        std::vector<int32_t> all;
+        D.all_own_off.assign(h->world + 1, 0);
+        for (int q = 0; q < h->world; ++q) {
+            D.all_own_off[q + 1] = D.all_own_off[q] + (q == 0 ? 0 : D.own_count[q]);
+            if (q > 0) all.insert(all.end(), per_rank[q].begin(), per_rank[q].end());
+        }
+        HIPCHK(h, D.all_own_orig.upload(all, s));
+        HIPCHK(h, D.xbuf.alloc(std::max<int64_t>((int64_t)all.size(), 1)));
+    } else {
+        HIPCHK(h, D.xbuf.alloc(std::max<int64_t>(D.n_own, 1)));
+    }
+    return UNO_KKT_OK;
+}
+
+// Subtree roots whose parent is a top front: their blocks (contribution blocks after the factor,
+// update vectors after the forward solve) go to rank 0 at the same offsets (same layout everywhere).
+template <class Off, class Size>
+int exchange_roots(uno_kkt_t h, double* base, Off off, Size size) {
+    const Partition& Pt = h->dist.part;
+    hipStream_t s = h->stream;
+    HIPCHK(h, h->comm->group_begin());
+    for (size_t k = 0; k < Pt.send_roots.size(); ++k) {
+        const int32_t f = Pt.send_roots[k];
+        const int src = Pt.root_rank[k];
+        const int64_t n = size(f);
+        if (src == 0 || n <= 0) continue;
+        if (h->rank == src) HIPCHK(h, h->comm->send(base + off(f), (size_t)n * sizeof(double), 0, s));
+        else if (h->rank == 0) HIPCHK(h, h->comm->recv(base + off(f), (size_t)n * sizeof(double), src, s));
+    }
+    HIPCHK(h, h->comm->group_end());
+    return UNO_KKT_OK;
+}
+
+// Distributed equilibration: rows of the rank's subtrees are complete on the rank (every entry of such
+// a row lies in one of its fronts) and are scanned as on one GPU; the top rows' partials from every
+// rank are combined with all-reduces (max for the scaling sweeps, sum for the row sums), and
+// ||A_pre||_inf is the all-reduced max.  Same values as the single-GPU scan (max is exact; the
+// row-sum additions of a top row are regrouped by rank).
+int dist_scale(uno_kkt_t h, ScanArgs SA) {
+    DistState& D = h->dist;
+    hipStream_t s = h->stream;
+    SA.list = D.own_new.p;
+    SA.n = D.n_own;
+    SA.long_rows = D.own_long.p;
+    SA.n_long = D.n_own_long;
+    SA.max_long = D.max_own_long;
+    PartArgs PA;
+    PA.nchunks = D.nchunks; PA.chunk_row = D.chunk_row.p; PA.chunk_begin = D.chunk_begin.p; PA.pslot = D.pslot.p;
+    PA.ppartner = D.ppartner.p; PA.trow_orig = D.top_orig.p; PA.uval = h->uval.p; PA.scale = h->scale.p;
+    PA.outT = D.outT.p;
+    const int64_t nt = D.n_top_rows;
+    auto top_pass = [&](int mode, double* out, RedOp op) -> int {
+        if (nt == 0) return UNO_KKT_OK;
+        HIPCHK(h, hipMemsetAsync(D.outT.p, 0, sizeof(double) * nt, s));
+        HIPCHK(h, launch_rowscan_part(PA, mode, s));
+        HIPCHK(h, h->comm->allreduce(D.outT.p, (size_t)nt, op, s));
+        HIPCHK(h, launch_scatter(D.outT.p, D.top_orig.p, out, nt, s));
+        return UNO_KKT_OK;
+    };
+    int rc;
+    for (int it = 0; it < h->scale_iters; ++it) {
+        SA.out = h->rmax.p;
+        HIPCHK(h, launch_rowscan(SA, it == 0 ? 0 : 1, s));
+        if ((rc = top_pass(it == 0 ? 0 : 1, h->rmax.p, RedOp::MaxF64)) != UNO_KKT_OK) return rc;
+        HIPCHK(h, launch_scale_update(h->rmax.p, h->scale.p, D.own_orig.p, D.n_own, it == 0, s));
+        HIPCHK(h, launch_scale_update(h->rmax.p, h->scale.p, D.top_orig.p, nt, it == 0, s));
+    }
+    if (h->scale_iters == 0) {
+        HIPCHK(h, hipMemsetAsync(h->rmax.p, 0, sizeof(double) * h->S.n, s));
+        HIPCHK(h, launch_scale_update(h->rmax.p, h->scale.p, nullptr, h->S.n, 1, s));
+    }
+    SA.out = h->rowsum.p;
+    HIPCHK(h, launch_rowscan(SA, 2, s));
+    if ((rc = top_pass(2, h->rowsum.p, RedOp::SumF64)) != UNO_KKT_OK) return rc;
+    HIPCHK(h, launch_normmax(h->rowsum.p, D.own_orig.p, D.n_own, h->anorm.p, s));
+    HIPCHK(h, launch_normmax(h->rowsum.p, D.top_orig.p, nt, h->anorm.p, s));
+    HIPCHK(h, h->comm->allreduce(h->anorm.p, 1, RedOp::MaxU64, s));
+    return UNO_KKT_OK;
+}
+
+// host-side all-reduce of a small vector (delayed-pivot rounds only)
+int allreduce_host(uno_kkt_t h, std::vector<unsigned long long>& v, RedOp op) {
+    if (h->world <= 1 || v.empty()) return UNO_KKT_OK;
+    HIPCHK(h, h->dist.tmp.alloc(v.size()));
+    HIPCHK(h, hipMemcpyAsync(h->dist.tmp.p, v.data(), v.size() * 8, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, h->comm->allreduce(h->dist.tmp.p, v.size(), op, h->stream));
+    HIPCHK(h, hipMemcpyAsync(v.data(), h->dist.tmp.p, v.size() * 8, hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return UNO_KKT_OK;
+}
+
+
 int finish_factorization(uno_kkt_t h) {
     if (!h->factor_enqueued) return h->factored ? UNO_KKT_OK : set_err(h, UNO_KKT_ERR_STATE, "no factorization");
     HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -177,15 +454,37 @@ int finish_factorization(uno_kkt_t h) {
         int64_t nd = (int64_t)std::min<unsigned long long>(c[6], (unsigned long long)h->S.n);
         bool need = c[5] != 0 || (h->delay_relaxed && nd > 0);
         if (!need) break;
-        std::vector<int32_t> dv(nd);
-        if (nd > 0) HIPCHK(h, hipMemcpy(dv.data(), h->delayed.p, sizeof(int32_t) * nd, hipMemcpyDeviceToHost));
+        std::vector<int32_t> dv;
+        if (h->world == 1) {
+            dv.resize(nd);
+            if (nd > 0) HIPCHK(h, hipMemcpy(dv.data(), h->delayed.p, sizeof(int32_t) * nd, hipMemcpyDeviceToHost));
+        } else {
+            // every rank applies the union of all ranks' delayed columns (same structure everywhere)
+            std::vector<unsigned long long> cnt(h->world, 0);
+            cnt[h->rank] = std::min<unsigned long long>(c[7], (unsigned long long)h->S.n);
+            int rc = allreduce_host(h, cnt, RedOp::SumU64);
+            if (rc != UNO_KKT_OK) return rc;
+            int64_t total = 0, mine_off = 0;
+            for (int q = 0; q < h->world; ++q) { if (q == h->rank) mine_off = total; total += (int64_t)cnt[q]; }
+            std::vector<int32_t> my((size_t)cnt[h->rank]);
+            if (!my.empty()) HIPCHK(h, hipMemcpy(my.data(), h->delayed.p, sizeof(int32_t) * my.size(), hipMemcpyDeviceToHost));
+            std::vector<unsigned long long> all((size_t)total, 0);
+            for (size_t q = 0; q < my.size(); ++q) all[mine_off + q] = (unsigned long long)my[q];
+            if ((rc = allreduce_host(h, all, RedOp::SumU64)) != UNO_KKT_OK) return rc;
+            for (unsigned long long v : all) dv.push_back((int32_t)v);
+        }
+        std::sort(dv.begin(), dv.end());  // deterministic merge order
         int64_t moved = delay_columns(h->P, h->S, dv);
         if (moved == 0) {
             // fall back to whole-front amalgamation for stuck fronts (cannot happen at roots)
             std::vector<int32_t> fs(h->S.nf);
-            HIPCHK(h, hipMemcpy(fs.data(), h->fstat.p, sizeof(int32_t) * fs.size(), hipMemcpyDeviceToHost));
+            if (h->S.nf > 0) HIPCHK(h, hipMemcpy(fs.data(), h->fstat.p, sizeof(int32_t) * fs.size(), hipMemcpyDeviceToHost));
+            std::vector<unsigned long long> stuck(h->S.nf);
+            for (int64_t f = 0; f < h->S.nf; ++f) stuck[f] = (fs[f] & 0xffff) != 0;
+            int rc = allreduce_host(h, stuck, RedOp::MaxU64);
+            if (rc != UNO_KKT_OK) return rc;
             std::vector<char> merge(h->S.nf, 0);
-            for (int64_t f = 0; f < h->S.nf; ++f) merge[f] = (fs[f] & 0xffff) != 0;
+            for (int64_t f = 0; f < h->S.nf; ++f) merge[f] = stuck[f] != 0;
             moved = amalgamate(h->P, h->S, merge);
         }
         if (moved == 0) break;
@@ -261,7 +560,6 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->L_off.upload(S.f_L_off, s));
     HIPCHK(h, h->cb_off.upload(S.f_cb_off, s));
     HIPCHK(h, h->gscratch_off.upload(goff, s));
-    HIPCHK(h, h->level_fronts.upload(S.level_fronts, s));
     HIPCHK(h, h->fstat.alloc(S.nf));
     HIPCHK(h, h->fcnt.alloc(S.nf));
     HIPCHK(h, h->perm_d.upload(S.perm, s));
@@ -283,6 +581,7 @@ int upload_structure(uno_kkt_t h) {
     if (h->uval.n != (size_t)S.nu) HIPCHK(h, h->uval.alloc(S.nu));
     if (h->scale.n != (size_t)n) {
         HIPCHK(h, h->scale.alloc(n));
+        if (n > 0) HIPCHK(h, hipMemsetAsync(h->scale.p, 0, sizeof(double) * n, s));  // rows of other ranks: x = 0
         HIPCHK(h, h->rowsum.alloc(n));
         HIPCHK(h, h->rmax.alloc(n));
         HIPCHK(h, h->w.alloc(n));
@@ -299,61 +598,20 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, h->anorm.alloc(1));
         HIPCHK(h, h->counters.alloc(8));
     }
-    // launch plan: per level, fronts sorted by order (descending) -> size classes
-    h->fac_launches.clear();
-    h->sol_launches.clear();
-    std::vector<int32_t> sfr;
-    sfr.reserve(S.nf);
-    for (int l = 0; l < S.nlevels; ++l) {
-        int b = S.level_off[l], e = S.level_off[l + 1];
-        {
-            std::vector<std::pair<int, int32_t>> wv;  // (LDS doubles, front)
-            std::vector<int32_t> big;
-            for (int q = b; q < e; ++q) {
-                const int32_t f = S.level_fronts[q];
-                const int m = S.f_m[f], p = S.f_p[f];
-                if (p <= 64 && m <= kMaxLdsFront) {
-                    const int sz = p * m - p * (p - 1) / 2;
-                    wv.push_back({((sz + 1) & ~1) + m, f});
-                } else {
-                    big.push_back(f);
-                }
-            }
-            std::sort(wv.begin(), wv.end(), [](const auto& x, const auto& y) { return x.first > y.first; });
-            size_t q = 0;
-            while (q < wv.size()) {
-                int cap = 256;
-                while (cap < wv[q].first) cap *= 2;
-                size_t r = q;
-                while (r < wv.size() && (wv[r].first > cap / 2 || cap == 256)) ++r;
-                SolveLaunch sl{l, (int)sfr.size(), (int)(r - q), wv[q].first, 0, 0, true};
-                for (size_t t = q; t < r; ++t) sfr.push_back(wv[t].second);
-                h->sol_launches.push_back(sl);
-                q = r;
-            }
-            if (!big.empty()) {
-                SolveLaunch sl{l, (int)sfr.size(), (int)big.size(), 0, 0, 0, false};
-                for (int32_t f : big) {
-                    sfr.push_back(f);
-                    sl.mmax = std::max(sl.mmax, S.f_m[f]);
-                    sl.pmax = std::max(sl.pmax, S.f_p[f]);
-                }
-                h->sol_launches.push_back(sl);
-            }
-        }
-        int q = b;
-        while (q < e) {
-            int m0 = S.f_m[S.level_fronts[q]];
-            bool global = m0 > kMaxLdsFront;
-            int cap = global ? 1 << 30 : (m0 > 64 ? kMaxLdsFront : (m0 > 32 ? 64 : 32));
-            int floor_ = global ? kMaxLdsFront : (cap == kMaxLdsFront ? 64 : (cap == 64 ? 32 : 0));
-            int r = q;
-            while (r < e && S.f_m[S.level_fronts[r]] > floor_ && S.f_m[S.level_fronts[r]] <= cap) ++r;
-            h->fac_launches.push_back({q, r - q, m0, global});
-            q = r;
-        }
+    if (S.nf > 0) {  // fronts another rank factors keep zero records
+        HIPCHK(h, hipMemsetAsync(h->fstat.p, 0, sizeof(int32_t) * S.nf, s));
+        HIPCHK(h, hipMemsetAsync(h->fcnt.p, 0, sizeof(unsigned long long) * S.nf, s));
     }
-    HIPCHK(h, h->solve_fronts.upload(sfr, s));
+    if (h->world > 1) {
+        int rc = setup_distribution(h);
+        if (rc != UNO_KKT_OK) return rc;
+        const Partition& Pt = h->dist.part;
+        HIPCHK(h, build_plan(h, [&](int32_t f) { return Pt.owner[f] == h->rank; }, h->plan[0]));
+        HIPCHK(h, build_plan(h, [&](int32_t f) { return h->rank == 0 && Pt.owner[f] < 0; }, h->plan[1]));
+    } else {
+        HIPCHK(h, build_plan(h, [](int32_t) { return true; }, h->plan[0]));
+        HIPCHK(h, build_plan(h, [](int32_t) { return false; }, h->plan[1]));
+    }
     HIPCHK(h, hipStreamSynchronize(s));
     double an = h->st.analysis_seconds;
     int64_t nfac = h->st.factorizations, nsol = h->st.solves;
@@ -382,16 +640,26 @@ int enqueue_factorization(uno_kkt_t h) {
     HIPCHK(h, hipMemsetAsync(h->anorm.p, 0, sizeof(unsigned long long), s));
     {
         TimerScope t(h, KC_PACK);
-        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, S.nu, h->uval.p, s));
+        if (h->world == 1) {
+            HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, 0, S.nu, h->uval.p, s));
+        } else {
+            for (const auto& r : h->dist.pack_ranges)
+                HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, r.first, r.second, h->uval.p, s));
+        }
     }
     {
         TimerScope t(h, KC_SCALE);
         ScanArgs SA;
-        SA.n = S.n; SA.perm = h->perm_d.p; SA.cptr = h->cptr.p; SA.rptr = h->rptr.p; SA.rslot = h->rslot.p;
-        SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p; SA.scale = h->scale.p; SA.out = nullptr;
-        SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p; SA.n_long = h->n_long;
-        SA.max_long = h->max_long;
-        HIPCHK(h, launch_scale(SA, h->scale_iters, h->rmax.p, h->rowsum.p, s));
+        SA.n = S.n; SA.list = nullptr; SA.perm = h->perm_d.p; SA.cptr = h->cptr.p; SA.rptr = h->rptr.p;
+        SA.rslot = h->rslot.p; SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p;
+        SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p;
+        SA.n_long = h->n_long; SA.max_long = h->max_long;
+        if (h->world == 1) {
+            HIPCHK(h, launch_scale(SA, h->scale_iters, h->rmax.p, h->rowsum.p, s));
+        } else {
+            int rc = dist_scale(h, SA);
+            if (rc != UNO_KKT_OK) return rc;
+        }
     }
     FactorArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
@@ -409,11 +677,26 @@ int enqueue_factorization(uno_kkt_t h) {
         HIPCHK(h, hipMemsetAsync(h->stamps.p, 0, sizeof(unsigned long long) * 8 * S.nf, s));
         A.stamps = h->stamps.p;
     }
-    for (const Launch& L : h->fac_launches) {
+    for (const Launch& L : h->plan[0].fac) {
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
-        HIPCHK(h, launch_factor(A, h->level_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+        HIPCHK(h, launch_factor(A, h->plan[0].fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+    }
+    if (h->world > 1) {
+        // subtree roots' contribution blocks -> rank 0 (same arena offsets on every rank)
+        int rc = exchange_roots(h, h->cb.p, [&](int32_t f) { return S.f_cb_off[f]; },
+                                [&](int32_t f) { return S.f_cb_off[f + 1] - S.f_cb_off[f]; });
+        if (rc != UNO_KKT_OK) return rc;
+        for (const Launch& L : h->plan[1].fac) {
+            TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
+            HIPCHK(h, launch_factor(A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+        }
     }
     HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, S.nf, h->counters.p, s));
+    if (h->world > 1) {
+        // counters[7] keeps this rank's delayed-column count; 0..6 are summed over the ranks
+        HIPCHK(h, hipMemcpyAsync(h->counters.p + 7, h->counters.p + 6, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
+        HIPCHK(h, h->comm->allreduce(h->counters.p, 7, RedOp::SumU64, s));
+    }
     HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     h->factor_enqueued = true;
     return UNO_KKT_OK;
@@ -451,6 +734,7 @@ void uno_kkt_destroy(uno_kkt_t h) {
     for (auto& t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
     if (h->h_counters) hipHostFree(h->h_counters);
+    delete h->comm;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
 }
@@ -468,6 +752,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
+    else if (n == "gather_solution") h->gather_solution = value != 0.0;
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;
 }
@@ -586,23 +871,61 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
     A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p;
-    auto run = [&](const SolveLaunch& L, bool forward) -> hipError_t {
-        const int32_t* fr = h->solve_fronts.p + L.begin;
+    auto run = [&](const Plan& P, const SolveLaunch& L, bool forward) -> hipError_t {
+        const int32_t* fr = P.sol_fronts.p + L.begin;
         return L.wave ? launch_solve_wave(A, fr, L.count, L.lds, forward, s)
                       : launch_solve(A, fr, L.count, L.mmax, L.pmax, forward, s);
     };
-    for (size_t q = 0; q < h->sol_launches.size(); ++q) {
+    const Plan& P0 = h->plan[0];
+    const Plan& P1 = h->plan[1];
+    for (size_t q = 0; q < P0.sol.size(); ++q) {
         TimerScope t(h, KC_SOLVE_FWD);
-        HIPCHK(h, run(h->sol_launches[q], true));
+        HIPCHK(h, run(P0, P0.sol[q], true));
     }
-    for (size_t q = h->sol_launches.size(); q-- > 0;) {
+    if (h->world > 1) {
+        DistState& D = h->dist;
+        // forward: subtree roots' update vectors -> rank 0, which solves the top of the tree
+        int rc = exchange_roots(h, h->cvec.p, [&](int32_t f) { return S.f_relmap_off[f]; },
+                                [&](int32_t f) { return (int64_t)(S.f_m[f] - S.f_p[f]); });
+        if (rc != UNO_KKT_OK) return rc;
+        for (size_t q = 0; q < P1.sol.size(); ++q) {
+            TimerScope t(h, KC_SOLVE_FWD);
+            HIPCHK(h, run(P1, P1.sol[q], true));
+        }
+        for (size_t q = P1.sol.size(); q-- > 0;) {
+            TimerScope t(h, KC_SOLVE_BWD);
+            HIPCHK(h, run(P1, P1.sol[q], false));
+        }
+        // backward: the top rows' solution is broadcast, then every rank finishes its subtrees
+        if (D.n_top_rows > 0) {
+            if (h->rank == 0) HIPCHK(h, launch_gather(h->w.p, D.top_orig.p, D.tbuf.p, D.n_top_rows, s));
+            HIPCHK(h, h->comm->broadcast(D.tbuf.p, sizeof(double) * D.n_top_rows, 0, s));
+            if (h->rank != 0) HIPCHK(h, launch_scatter(D.tbuf.p, D.top_orig.p, h->w.p, D.n_top_rows, s));
+        }
+    }
+    for (size_t q = P0.sol.size(); q-- > 0;) {
         TimerScope t(h, KC_SOLVE_BWD);
-        HIPCHK(h, run(h->sol_launches[q], false));
+        HIPCHK(h, run(P0, P0.sol[q], false));
     }
     double* xd = on_device ? x : h->bvec.p;
     {
         TimerScope t(h, KC_RHS);
         HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
+    }
+    if (h->world > 1 && h->gather_solution) {
+        // MUMPS-style centralized solution on rank 0 (ICNTL(21) = 0): own rows of every other rank
+        DistState& D = h->dist;
+        if (h->rank != 0 && D.n_own > 0) HIPCHK(h, launch_gather(xd, D.own_orig.p, D.xbuf.p, D.n_own, s));
+        HIPCHK(h, h->comm->group_begin());
+        for (int q = 1; q < h->world; ++q) {
+            const int64_t k = D.own_count[q];
+            if (k == 0) continue;
+            if (h->rank == q) HIPCHK(h, h->comm->send(D.xbuf.p, sizeof(double) * k, 0, s));
+            else if (h->rank == 0) HIPCHK(h, h->comm->recv(D.xbuf.p + D.all_own_off[q], sizeof(double) * k, q, s));
+        }
+        HIPCHK(h, h->comm->group_end());
+        if (h->rank == 0)
+            HIPCHK(h, launch_scatter(D.xbuf.p, D.all_own_orig.p, xd, D.all_own_off[h->world], s));
     }
     h->st.solves++;
     if (!on_device) {
@@ -652,6 +975,20 @@ int uno_kkt_reset_kernel_times(uno_kkt_t h) {
 
 void* uno_kkt_stream(uno_kkt_t h) { return h ? (void*)h->stream : nullptr; }
 
+// diagnostics (include/uno_kkt_debug.h): host-only analysis + subtree partition (no device needed)
+int64_t uno_kkt_debug_partition(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int world,
+                                int32_t* owner, int32_t* parent, int64_t cap, int64_t* n_subtrees) {
+    Pattern P;
+    Symbolic S;
+    if (!ukkt::analyze(n, nnz, row, col, AnalysisOptions(), P, S).empty()) return -1;
+    Partition Pt;
+    partition_tree(S, world, Pt);
+    if (cap < S.nf) return -S.nf;
+    for (int64_t f = 0; f < S.nf; ++f) { owner[f] = Pt.owner[f]; parent[f] = S.f_parent[f]; }
+    if (n_subtrees) *n_subtrees = Pt.n_subtrees;
+    return S.nf;
+}
+
 // diagnostics (include/uno_kkt_debug.h): per-front phase stamps of the last factorization
 int64_t uno_kkt_debug_stamps(uno_kkt_t h, uint64_t* out, int64_t cap, int32_t* fm, int32_t* fp, int32_t* flevel) {
     if (!h || !h->stamps.p) return -1;
@@ -664,5 +1001,62 @@ int64_t uno_kkt_debug_stamps(uno_kkt_t h, uint64_t* out, int64_t cap, int32_t* f
 }
 
 const char* uno_kkt_last_error(uno_kkt_t h) { return h ? h->err.c_str() : "null handle"; }
+
+// ---- distributed factorization ----
+int uno_kkt_comm_unique_id(unsigned char id[128]) {
+    if (!id) return UNO_KKT_ERR_ARG;
+    return ukkt::rccl_unique_id(id) == 0 ? UNO_KKT_OK : UNO_KKT_ERR_HIP;
+}
+
+static int attach(uno_kkt_t h, ukkt::Transport* t) {
+    delete h->comm;
+    h->comm = t;
+    h->rank = t->rank();
+    h->world = t->size();
+    h->analyzed = h->factored = h->factor_enqueued = false;
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_attach_rccl(uno_kkt_t h, const unsigned char id[128], int rank, int world) {
+    if (!h || !id || world < 1 || rank < 0 || rank >= world) return UNO_KKT_ERR_ARG;
+    std::string err;
+    ukkt::Transport* t = ukkt::make_rccl_transport(id, rank, world, h->device, err);
+    if (!t) return set_err(h, UNO_KKT_ERR_HIP, err);
+    return attach(h, t);
+}
+
+int uno_kkt_group_create(uno_kkt_group_t* g, int world) {
+    if (!g || world < 1) return UNO_KKT_ERR_ARG;
+    *g = reinterpret_cast<uno_kkt_group_t>(ukkt::local_group_create(world));
+    return UNO_KKT_OK;
+}
+
+void uno_kkt_group_destroy(uno_kkt_group_t g) { ukkt::local_group_destroy(reinterpret_cast<ukkt::LocalGroup*>(g)); }
+
+int uno_kkt_attach_local(uno_kkt_t h, uno_kkt_group_t g, int rank) {
+    if (!h || !g) return UNO_KKT_ERR_ARG;
+    ukkt::Transport* t = ukkt::make_local_transport(reinterpret_cast<ukkt::LocalGroup*>(g), rank);
+    if (!t) return set_err(h, UNO_KKT_ERR_ARG, "bad rank for local group");
+    return attach(h, t);
+}
+
+int uno_kkt_dist_info(uno_kkt_t h, uno_kkt_dist_info_t* out) {
+    if (!h || !out) return UNO_KKT_ERR_ARG;
+    memset(out, 0, sizeof(*out));
+    out->rank = h->rank;
+    out->world = h->world;
+    if (h->world > 1 && h->analyzed) {
+        const DistState& D = h->dist;
+        out->subtrees = D.part.n_subtrees;
+        out->top_fronts = D.part.n_top;
+        out->my_fronts = D.my_fronts;
+        out->own_rows = D.n_own;
+        out->top_rows = D.n_top_rows;
+        out->my_flops = D.my_flops;
+        out->top_flops = D.top_flops;
+        out->est_imbalance = D.part.total_work > 0 ? D.part.max_rank_work * h->world / D.part.total_work : 1.0;
+    }
+    return UNO_KKT_OK;
+}
 
 }  // extern "C"

@@ -31,8 +31,8 @@ __device__ __forceinline__ unsigned long long as_bits(double d) { return (unsign
 // ------------------------------------------------------------------------------------------------
 
 __global__ void k_pack(const double* __restrict__ values, const int32_t* __restrict__ dup_ptr,
-                       const int32_t* __restrict__ dup_pos, int64_t nu, double* __restrict__ uval) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nu; s += (int64_t)gridDim.x * blockDim.x) {
+                       const int32_t* __restrict__ dup_pos, int64_t begin, int64_t end, double* __restrict__ uval) {
+    for (int64_t s = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < end; s += (int64_t)gridDim.x * blockDim.x) {
         double v;
         if (dup_ptr == nullptr) {
             v = values[dup_pos[s]];
@@ -83,7 +83,7 @@ __global__ void k_rowscan(ScanArgs A) {
     const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16;
     const int lane = threadIdx.x & 15;
     if (g >= A.n) return;
-    const int32_t i = (int32_t)g;
+    const int32_t i = A.list ? A.list[g] : (int32_t)g;
     if ((A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > kLongRow) {
         if (lane == 0) A.out[A.perm[i]] = 0.0;  // combined by k_rowscan_long
         return;
@@ -125,12 +125,54 @@ __global__ void k_rowscan_long(ScanArgs A) {
     }
 }
 
+// Partial row scans of the separator ("top") rows on one rank of a distributed factorization: the
+// rank's own slots of each top row, cut into chunks (one workgroup each), combined per row with one
+// atomic per workgroup; the ranks' partials are then all-reduced (max / sum) over the top rows.
+template <int MODE>
+__global__ void k_rowscan_part(PartArgs A) {
+    __shared__ double red[kThreads / 64];
+    const int64_t c = blockIdx.x;
+    const int32_t t = A.chunk_row[c];
+    const int32_t orig = A.trow_orig[t];
+    const double si = MODE > 0 ? A.scale[orig] : 1.0;
+    double acc = 0.0;
+    for (int64_t q = A.chunk_begin[c] + threadIdx.x; q < A.chunk_begin[c + 1]; q += kThreads) {
+        const int32_t slot = A.pslot[q];
+        const double w = MODE == 0 ? fabs(A.uval[slot]) : fabs(si * A.uval[slot] * A.scale[A.ppartner[q]]);
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        double o = __shfl_xor(acc, off);
+        acc = MODE == 2 ? acc + o : fmax(acc, o);
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kThreads / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
+        if (MODE == 2) atomicAdd(A.outT + t, acc);
+        else atomicMax((unsigned long long*)(A.outT + t), as_bits(acc));  // non-negative doubles
+    }
+}
+
+__global__ void k_scatter(const double* __restrict__ src, const int32_t* __restrict__ idx, double* __restrict__ dst,
+                          int64_t k) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x)
+        dst[idx[t]] = src[t];
+}
+
+__global__ void k_gather(const double* __restrict__ src, const int32_t* __restrict__ idx, double* __restrict__ dst,
+                         int64_t k) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x)
+        dst[t] = src[idx[t]];
+}
+
 // ||A_pre||_inf = max_i rowsum_i: grid-stride block maxima, one atomic per workgroup
-__global__ void k_normmax(const double* __restrict__ rowsum, int64_t n, unsigned long long* __restrict__ anorm) {
+__global__ void k_normmax(const double* __restrict__ rowsum, const int32_t* __restrict__ list, int64_t n,
+                          unsigned long long* __restrict__ anorm) {
     __shared__ double red[kThreads / 64];
     double mx = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
-        mx = fmax(mx, rowsum[i]);
+        mx = fmax(mx, rowsum[list ? list[i] : i]);
     for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
     __syncthreads();
@@ -140,8 +182,10 @@ __global__ void k_normmax(const double* __restrict__ rowsum, int64_t n, unsigned
     }
 }
 
-__global__ void k_scale_update(const double* __restrict__ rmax, double* __restrict__ scale, int64_t n, int first) {
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+__global__ void k_scale_update(const double* __restrict__ rmax, double* __restrict__ scale, const int32_t* __restrict__ list,
+                               int64_t n, int first) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = list ? list[t] : t;
         double r = rmax[i];
         double s = first ? 1.0 : scale[i];
         if (r > 0.0) s = s / sqrt(r);
@@ -1175,42 +1219,80 @@ static int grid_for(int64_t n, int block) {
     return (int)g;
 }
 
-hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t nu, double* uval,
-                       hipStream_t s) {
-    if (nu == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(nu, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, nu, uval);
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t begin, int64_t end,
+                       double* uval, hipStream_t s) {
+    if (end <= begin) return hipSuccess;
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(end - begin, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, begin, end, uval);
     return hipGetLastError();
 }
 
-template <int MODE>
-static void scan(const ScanArgs& A, hipStream_t s) {
-    const int64_t threads = A.n * 16;
-    hipLaunchKernelGGL(k_rowscan<MODE>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A);
+hipError_t launch_rowscan(const ScanArgs& A, int mode, hipStream_t s) {
+    if (A.n > 0) {
+        const int64_t threads = A.n * 16;
+        const dim3 g((unsigned)((threads + 255) / 256));
+        if (mode == 0) hipLaunchKernelGGL(k_rowscan<0>, g, dim3(256), 0, s, A);
+        else if (mode == 1) hipLaunchKernelGGL(k_rowscan<1>, g, dim3(256), 0, s, A);
+        else hipLaunchKernelGGL(k_rowscan<2>, g, dim3(256), 0, s, A);
+    }
     if (A.n_long > 0) {
-        hipLaunchKernelGGL(k_rowscan_long<MODE>, dim3((unsigned)((A.max_long + kLongChunk - 1) / kLongChunk), A.n_long),
-                           dim3(kThreads), 0, s, A);
+        const dim3 g((unsigned)((A.max_long + kLongChunk - 1) / kLongChunk), A.n_long);
+        if (mode == 0) hipLaunchKernelGGL(k_rowscan_long<0>, g, dim3(kThreads), 0, s, A);
+        else if (mode == 1) hipLaunchKernelGGL(k_rowscan_long<1>, g, dim3(kThreads), 0, s, A);
+        else hipLaunchKernelGGL(k_rowscan_long<2>, g, dim3(kThreads), 0, s, A);
     }
-    if (MODE == 2) {
-        int g = grid_for(A.n, kThreads);
-        hipLaunchKernelGGL(k_normmax, dim3(g > 512 ? 512 : g), dim3(kThreads), 0, s, A.out, A.n, A.anorm);
-    }
+    return hipGetLastError();
+}
+
+hipError_t launch_rowscan_part(const PartArgs& A, int mode, hipStream_t s) {
+    if (A.nchunks <= 0) return hipSuccess;
+    const dim3 g((unsigned)A.nchunks);
+    if (mode == 0) hipLaunchKernelGGL(k_rowscan_part<0>, g, dim3(kThreads), 0, s, A);
+    else if (mode == 1) hipLaunchKernelGGL(k_rowscan_part<1>, g, dim3(kThreads), 0, s, A);
+    else hipLaunchKernelGGL(k_rowscan_part<2>, g, dim3(kThreads), 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_scale_update(const double* rmax, double* scale, const int32_t* list, int64_t n, int first, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scale_update, dim3(grid_for(n, 256)), dim3(256), 0, s, rmax, scale, list, n, first);
+    return hipGetLastError();
+}
+
+hipError_t launch_normmax(const double* rowsum, const int32_t* list, int64_t n, unsigned long long* anorm, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    int g = grid_for(n, kThreads);
+    hipLaunchKernelGGL(k_normmax, dim3(g > 512 ? 512 : g), dim3(kThreads), 0, s, rowsum, list, n, anorm);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter, dim3(grid_for(k, 256)), dim3(256), 0, s, src, idx, dst, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gather, dim3(grid_for(k, 256)), dim3(256), 0, s, src, idx, dst, k);
+    return hipGetLastError();
 }
 
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     for (int it = 0; it < iters; ++it) {
         A.out = rmax;
-        if (it == 0) scan<0>(A, s);
-        else scan<1>(A, s);
-        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(A.n, 256)), dim3(256), 0, s, rmax, A.scale, A.n, it == 0 ? 1 : 0);
+        hipError_t e = launch_rowscan(A, it == 0 ? 0 : 1, s);
+        if (e != hipSuccess) return e;
+        if ((e = launch_scale_update(rmax, A.scale, nullptr, A.n, it == 0 ? 1 : 0, s)) != hipSuccess) return e;
     }
     if (iters == 0) {  // no scaling: s = 1
         hipMemsetAsync(rmax, 0, sizeof(double) * A.n, s);
-        hipLaunchKernelGGL(k_scale_update, dim3(grid_for(A.n, 256)), dim3(256), 0, s, rmax, A.scale, A.n, 1);
+        launch_scale_update(rmax, A.scale, nullptr, A.n, 1, s);
     }
     A.out = rowsum;
-    scan<2>(A, s);
-    return hipGetLastError();
+    hipError_t e = launch_rowscan(A, 2, s);
+    if (e != hipSuccess) return e;
+    return launch_normmax(rowsum, nullptr, A.n, A.anorm, s);
 }
 
 size_t factor_lds_bytes(int mmax) {

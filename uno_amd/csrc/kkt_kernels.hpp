@@ -65,7 +65,8 @@ struct SolveArgs {
 
 // row-wise scans for the equilibration and ||A_pre||_inf (kkt_kernels.hip k_rowscan)
 struct ScanArgs {
-    int64_t n;
+    int64_t n;               // rows to scan (list entries, or rows 0..n-1 when list is null)
+    const int32_t* list;     // optional row list (new numbering): a rank's own rows
     const int32_t* perm;     // new -> original
     const int32_t* cptr;     // n+1 column part of each row (contiguous slots)
     const int32_t* rptr;     // n+1 row part
@@ -81,11 +82,34 @@ struct ScanArgs {
     int64_t max_long;          // longest row length among long_rows
 };
 constexpr int kLongRow = 2048;
+
+// partial scans of the top (separator) rows on one rank: chunk c covers pslot[chunk_begin[c] ..
+// chunk_begin[c+1]) of top row chunk_row[c]; ppartner = original id of the slot's other index
+struct PartArgs {
+    int64_t nchunks;
+    const int32_t* chunk_row;
+    const int64_t* chunk_begin;  // nchunks+1
+    const int32_t* pslot;
+    const int32_t* ppartner;
+    const int32_t* trow_orig;    // top row t -> original id
+    const double* uval;
+    const double* scale;
+    double* outT;                // per top row
+};
 constexpr int kLongChunk = 4096;
 
-hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t nu, double* uval,
-                       hipStream_t s);
+// pack slots [begin, end)
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t begin, int64_t end,
+                       double* uval, hipStream_t s);
+// single-GPU equilibration: `iters` max-scaling sweeps over all rows, then row sums and ||A_pre||_inf
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s);
+// building blocks of the distributed equilibration (mode 0: max |a|, 1: max |s a s|, 2: sum |s a s|)
+hipError_t launch_rowscan(const ScanArgs& A, int mode, hipStream_t s);
+hipError_t launch_rowscan_part(const PartArgs& A, int mode, hipStream_t s);
+hipError_t launch_scale_update(const double* rmax, double* scale, const int32_t* list, int64_t n, int first, hipStream_t s);
+hipError_t launch_normmax(const double* rowsum, const int32_t* list, int64_t n, unsigned long long* anorm, hipStream_t s);
+hipError_t launch_scatter(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s);  // dst[idx[t]] = src[t]
+hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s);   // dst[t] = src[idx[t]]
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 // one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of

@@ -17,6 +17,7 @@ LIB_PATH = os.path.join(_HERE, "libuno_kkt.so")
 GEN_PATH = os.path.join(_HERE, "libarrowband.so")
 
 UNO_KKT_OK = 0
+UNO_KKT_ERR_ARG = -1
 _ERR_NAMES = {-1: "ERR_ARG", -2: "ERR_STATE", -3: "ERR_HIP", -4: "ERR_PIVOT", -5: "ERR_NOMEM", -6: "ERR_NODEVICE"}
 
 _i64p = ctypes.POINTER(ctypes.c_int64)
@@ -41,8 +42,21 @@ EXPORTED_SYMBOLS = [
     "uno_kkt_create", "uno_kkt_destroy", "uno_kkt_set_option", "uno_kkt_analyze", "uno_kkt_factorize",
     "uno_kkt_set_values", "uno_kkt_fill_values", "uno_kkt_inertia", "uno_kkt_solve", "uno_kkt_stats",
     "uno_kkt_kernel_times", "uno_kkt_reset_kernel_times", "uno_kkt_stream", "uno_kkt_last_error",
-    "uno_kkt_version",
+    "uno_kkt_version", "uno_kkt_comm_unique_id", "uno_kkt_attach_rccl", "uno_kkt_group_create",
+    "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info",
 ]
+
+
+class KKTDistInfo(ctypes.Structure):
+    _fields_ = [
+        ("rank", ctypes.c_int64), ("world", ctypes.c_int64), ("subtrees", ctypes.c_int64),
+        ("top_fronts", ctypes.c_int64), ("my_fronts", ctypes.c_int64), ("own_rows", ctypes.c_int64),
+        ("top_rows", ctypes.c_int64), ("my_flops", ctypes.c_double), ("top_flops", ctypes.c_double),
+        ("est_imbalance", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 _lib = None
 
@@ -74,6 +88,16 @@ def load_library():
     lib.uno_kkt_last_error.argtypes = [vp]
     lib.uno_kkt_last_error.restype = ctypes.c_char_p
     lib.uno_kkt_version.restype = ctypes.c_char_p
+    lib.uno_kkt_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.uno_kkt_attach_rccl.argtypes = [vp, ctypes.c_char_p, ctypes.c_int, ctypes.c_int]
+    lib.uno_kkt_group_create.argtypes = [ctypes.POINTER(vp), ctypes.c_int]
+    lib.uno_kkt_group_destroy.argtypes = [vp]
+    lib.uno_kkt_group_destroy.restype = None
+    lib.uno_kkt_attach_local.argtypes = [vp, vp, ctypes.c_int]
+    lib.uno_kkt_dist_info.argtypes = [vp, ctypes.POINTER(KKTDistInfo)]
+    lib.uno_kkt_debug_partition.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int,
+                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _i64p]
+    lib.uno_kkt_debug_partition.restype = ctypes.c_int64
     _lib = lib
     return lib
 
@@ -183,6 +207,64 @@ class HipKKT:
 
     def reset_kernel_times(self):
         self._check(self.lib.uno_kkt_reset_kernel_times(self.h))
+
+    # ---- multi-GPU (one factorization partitioned over ranks; attach before analyze) ----
+    def attach_rccl(self, unique_id, rank, world):
+        self._check(self.lib.uno_kkt_attach_rccl(self.h, bytes(unique_id), int(rank), int(world)))
+
+    def attach_local(self, group, rank):
+        self._check(self.lib.uno_kkt_attach_local(self.h, group.g, int(rank)))
+
+    def dist_info(self):
+        d = KKTDistInfo()
+        self._check(self.lib.uno_kkt_dist_info(self.h, ctypes.byref(d)))
+        return d.as_dict()
+
+
+def rccl_unique_id():
+    """ncclGetUniqueId (128 bytes) for uno_kkt_attach_rccl; call on rank 0 and share out of band."""
+    lib = load_library()
+    buf = ctypes.create_string_buffer(128)
+    rc = lib.uno_kkt_comm_unique_id(buf)
+    if rc != UNO_KKT_OK:
+        raise KKTError(rc, "ncclGetUniqueId failed")
+    return buf.raw
+
+
+class LocalGroup:
+    """In-process group of `world` ranks (one host thread per rank, e.g. several ranks on one GPU)."""
+
+    def __init__(self, world):
+        self.lib = load_library()
+        self.g = ctypes.c_void_p()
+        rc = self.lib.uno_kkt_group_create(ctypes.byref(self.g), int(world))
+        if rc != UNO_KKT_OK:
+            raise KKTError(rc, "group create failed")
+        self.world = int(world)
+
+    def close(self):
+        if getattr(self, "g", None):
+            self.lib.uno_kkt_group_destroy(self.g)
+            self.g = None
+
+    def __del__(self):
+        self.close()
+
+
+def debug_partition(n, rows, cols, world):
+    """Host-only analysis + subtree partition: (owner per front (-1 = top), parent per front, subtrees)."""
+    lib = load_library()
+    r, rp = _i64(rows)
+    c, cp = _i64(cols)
+    cap = max(16, int(n))
+    owner = np.zeros(cap, dtype=np.int32)
+    parent = np.zeros(cap, dtype=np.int32)
+    ns = ctypes.c_int64()
+    nf = lib.uno_kkt_debug_partition(int(n), len(r), rp, cp, int(world), owner.ctypes.data_as(ctypes.c_void_p),
+                                     parent.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(ns))
+    if nf < 0:
+        raise KKTError(UNO_KKT_ERR_ARG if nf == -1 else nf, "debug_partition failed")
+    return owner[:nf].copy(), parent[:nf].copy(), ns.value
 
 
 # ---------------------------------------------------------------------------------------------

@@ -1,5 +1,4 @@
-"""Timing harness for the multi-GPU bench (independent KKT systems,
-one per rank, no data-path collective).
+"""Timing harness for the multi-GPU bench.
 
 The only collectives are the barriers bracketing the timed region and one MAX all-reduce of the
 per-rank elapsed time; `value` is then all ranks' factor+solves / that max.  Kept free of GPU calls
@@ -32,6 +31,16 @@ def timed_steps(step, steps, warmup, sync, world, device=None):
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item()), out
+
+
+def share_bytes(payload, world):
+    """Broadcast a small bytes object from rank 0 (the RCCL unique id of the library's communicator)."""
+    import torch.distributed as dist
+    if world <= 1:
+        return payload
+    box = [payload]
+    dist.broadcast_object_list(box, src=0)
+    return box[0]
 
 
 def aggregate(steps, world, elapsed):
