@@ -14,6 +14,9 @@ extern "C" {
  * -nf if cap is too small, -1 on a bad pattern. */
 int64_t uno_kkt_debug_partition(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int world,
                                 int32_t* owner, int32_t* parent, int64_t cap, int64_t* n_subtrees);
+/* Host-only symbolic analysis: per front its order, fully-summed columns and assembly-tree level. */
+int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int32_t* front_order,
+                             int32_t* front_pivots, int32_t* front_level, int64_t cap);
 int64_t uno_kkt_debug_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap, int32_t* front_order,
                              int32_t* front_pivots, int32_t* front_level);
 #ifdef __cplusplus

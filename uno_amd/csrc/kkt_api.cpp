@@ -249,15 +249,36 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
         }
         const int base = (int)ffr.size();
         ffr.insert(ffr.end(), lv.begin(), lv.end());
+        // factor launches: one per kernel instance and level (the launch reserves LDS for its largest
+        // front).  Finer LDS classes ({16, 24, .., 128}) were measured slower on C3 (2.36 vs 1.99 ms):
+        // the one-wave kernel is VALU-issue bound at levels 0-1 and more co-resident fronts per CU
+        // only lengthen every front; a class smaller than kMinClass absorbs the next smaller one.
+        static const int caps[] = {32, 64, 128};
+        constexpr int kMinClass = 2048;
+        auto prev_cap = [](int c) {
+            int pc = 0;
+            for (int x : caps) if (x < c) pc = x;
+            return pc;
+        };
+        auto kernel_of = [](int mm) { return mm > kMaxLdsFront ? 3 : (mm > 64 ? 2 : (mm > 32 ? 1 : 0)); };
         const int e = (int)lv.size();
         int q = 0;
         while (q < e) {
-            int m0 = S.f_m[lv[q]];
-            bool global = m0 > kMaxLdsFront;
-            int cap = global ? 1 << 30 : (m0 > 64 ? kMaxLdsFront : (m0 > 32 ? 64 : 32));
-            int floor_ = global ? kMaxLdsFront : (cap == kMaxLdsFront ? 64 : (cap == 64 ? 32 : 0));
+            const int m0 = S.f_m[lv[q]];
+            const bool global = m0 > kMaxLdsFront;
             int r = q;
-            while (r < e && S.f_m[lv[r]] > floor_ && S.f_m[lv[r]] <= cap) ++r;
+            if (global) {
+                while (r < e && S.f_m[lv[r]] > kMaxLdsFront) ++r;
+            } else {
+                int cap = 16;
+                for (int x : caps) if (x < m0) cap = x;  // largest cap below m0 ...
+                int floor_ = cap < m0 ? cap : 0;         // ... is the class floor
+                while (true) {
+                    while (r < e && S.f_m[lv[r]] > floor_) ++r;
+                    if (r >= e || r - q >= kMinClass || floor_ == 0 || kernel_of(S.f_m[lv[r]]) != kernel_of(m0)) break;
+                    floor_ = prev_cap(floor_);
+                }
+            }
             P.fac.push_back({base + q, r - q, m0, global});
             q = r;
         }
@@ -986,6 +1007,17 @@ int64_t uno_kkt_debug_partition(int64_t n, int64_t nnz, const int64_t* row, cons
     if (cap < S.nf) return -S.nf;
     for (int64_t f = 0; f < S.nf; ++f) { owner[f] = Pt.owner[f]; parent[f] = S.f_parent[f]; }
     if (n_subtrees) *n_subtrees = Pt.n_subtrees;
+    return S.nf;
+}
+
+// diagnostics (include/uno_kkt_debug.h): host-only analysis, per front order / pivots / level
+int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int32_t* fm, int32_t* fp,
+                             int32_t* flevel, int64_t cap) {
+    Pattern P;
+    Symbolic S;
+    if (!ukkt::analyze(n, nnz, row, col, AnalysisOptions(), P, S).empty()) return -1;
+    if (cap < S.nf) return -S.nf;
+    for (int64_t f = 0; f < S.nf; ++f) { fm[f] = S.f_m[f]; fp[f] = S.f_p[f]; flevel[f] = S.f_level[f]; }
     return S.nf;
 }
 

@@ -247,6 +247,13 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long x, i
     return ((unsigned long long)hi << 32) | lo;
 }
 __device__ __forceinline__ double readlane_d(double x, int l) { return as_double(readlane64(as_bits(x), l)); }
+// x of lane `src` (any lane pattern, one LDS-crossbar round trip, no LDS allocation, no barrier)
+__device__ __forceinline__ double bperm_d(double x, int src) {
+    const unsigned long long b = as_bits(x);
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)(b >> 32));
+    return as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
+}
 __device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 // max over the 64 lanes of a wave (every lane must be active)
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
@@ -502,12 +509,75 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // the LDS step below (search, interchanges, 1x1/2x2/null, Schur update) and reloads
     double R[RM][RM];
     double* colv = coefB;  // free until the write-out
+    // one-wave register path: columns whose L was written during the pivot loop (wave-uniform);
+    // cleared by any later symmetric interchange (their rows moved: rewritten from LDS at the end)
+    unsigned long long fastmask = 0;
+    bool spilled = false;  // some step ran the LDS path: the LDS front is current after the loop
+    double* Lf = A.L + A.L_off[f];
     if constexpr (REG) {
         if (W > 1 && tid == 0) sh->failk = -1;
         reg_load<G, RM>(st, m, R);
     }
     while (k < p) {
-        if constexpr (REG) {
+        if constexpr (REG && W == 1) {
+            // One wave owns the whole front (m <= G * RM): column k lives in the lanes with tx = k % G.
+            // Its entries are fetched straight from those lanes' registers with ds_bpermute (one
+            // crossbar round trip, no LDS store, no barrier), the threshold test is one ballot and the
+            // rank-1 update stays in registers; column k itself is left untouched, so L is written
+            // from the registers after the loop.
+            const int ty = tid / G, tx = tid % G;
+            const int nb = (m + G - 1) / G;  // row blocks holding front rows
+            bool need = false;
+#pragma unroll
+            for (int bk = 0; bk < RM; ++bk) {
+                while (!need && k < p && k / G == bk) {
+                    if (stamping) t_mark = __builtin_amdgcn_s_memtime();
+                    const int kk = k - G * bk;
+                    double lv[RM], cv[RM];
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) {
+                        if (a >= nb) break;  // uniform: row blocks beyond the front
+                        lv[a] = bperm_d(R[a][bk], ty * G + kk);  // A(ty + G a, k)
+                        cv[a] = bperm_d(R[a][bk], tx * G + kk);  // A(tx + G a, k)
+                    }
+                    const double akk = readlane_d(R[bk][bk], kk * G + kk);
+                    const double aak = fabs(akk);
+                    bool bad = !(aak > thres);
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) {
+                        if (a >= nb) break;
+                        const int i = ty + G * a, j = tx + G * a;
+                        lv[a] = (i > k && i < m) ? lv[a] : 0.0;
+                        cv[a] = (j > k && j < m) ? cv[a] : 0.0;
+                        bad |= A.u * fabs(lv[a]) > aak;
+                    }
+                    need = __ballot(bad) != 0;
+                    if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
+                    if (!need) {  // 1x1 pivot at k without interchange
+                        const double dinv = 1.0 / akk;
+#pragma unroll
+                        for (int b = bk; b < RM; ++b) {
+                            if (b >= nb) break;
+                            cv[b] *= dinv;
+                        }
+#pragma unroll
+                        for (int a = bk; a < RM; ++a) {
+                            if (a >= nb) break;
+#pragma unroll
+                            for (int b = bk; b <= a; ++b) R[a][b] -= lv[a] * cv[b];
+                        }
+                        if (tid == 0) { piv[k] = PIV_1X1; if (akk > 0.0) npos++; else nneg++; }
+                        fastmask |= 1ull << k;
+                        if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; }
+                        k += 1;
+                    }
+                }
+            }
+            if (!need) break;
+            spilled = true;
+            reg_store<G, RM>(st, m, R);
+            __syncthreads();
+        } else if constexpr (REG) {
             const int ty = tid / G, tx = tid % G;
             bool need = false;
 #pragma unroll
@@ -591,12 +661,14 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         if (d.c != k) {
             sym_swap<NT>(st, m, k, d.c, lrow, lorig);
             __syncthreads();
+            fastmask = 0;
         }
         if (d.kind == PIV_2X2_A) {
             int r = d.r == k ? d.c : d.r;
             if (r != k + 1) {
                 sym_swap<NT>(st, m, k + 1, r, lrow, lorig);
                 __syncthreads();
+                fastmask = 0;
             }
         }
         if (tid == 0) {
@@ -643,9 +715,35 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         if constexpr (REG) reg_load<G, RM>(st, m, R);
     }
     if constexpr (REG) {
-        reg_store<G, RM>(st, m, R);
-        __syncthreads();
+        if (W > 1 || spilled) {  // the write-out below reads the LDS front
+            reg_store<G, RM>(st, m, R);
+            __syncthreads();
+        }
     }
+    if constexpr (REG && W == 1) {
+        // L of the columns pivoted by the register path: column j (< p) still holds A(i, j) as it
+        // was at step j, so L(i, j) = A(i, j) / d_j and L(j, j) = d_j, stored straight from the
+        // registers (for a fixed register, the 8 lanes of a column group write 8 consecutive rows)
+        if (fastmask) {
+            const int ty = tid / G, tx = tid % G;
+#pragma unroll
+            for (int b = 0; b < RM; ++b) {
+                if (G * b >= p) break;  // uniform
+                const int j = tx + G * b;
+                const double dj = bperm_d(R[b][b], tx * (G + 1));  // A(j, j): lane (tx, tx)
+                const bool colok = j < p && ((fastmask >> (j & 63)) & 1);
+                const double djinv = 1.0 / dj;
+                double* Lj = Lf + (int64_t)j * m - (int64_t)j * (j - 1) / 2 - j;  // L(i, j) = Lj[i]
+#pragma unroll
+                for (int a = b; a < RM; ++a) {
+                    const int i = ty + G * a;
+                    if (colok && i >= j && i < m) Lj[i] = i == j ? dj : R[a][b] * djinv;
+                }
+            }
+        }
+    }
+    // columns still to be written from the LDS front (all when no register path ran)
+    const bool lds_L = !(REG && W == 1) || fastmask != (p >= 64 ? ~0ull : ((1ull << p) - 1));
     const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
@@ -659,7 +757,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // ---- write L: packed lower trapezoid, column j rows j..m-1 ----
     // per-column coefficients first (one division per column, not per entry):
     // L(i,j) = cA[j] * A(i,base) + cB[j] * A(i,base+1), base = j (1x1, 2x2 first) or j-1 (2x2 second)
-    for (int j = tid; j < p; j += NT) {
+    for (int j = tid; j < p && lds_L; j += NT) {
         const int8_t kind = piv[j];
         double ca = 0.0, cbv = 0.0;
         if (kind == PIV_1X1) {
@@ -676,8 +774,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     __syncthreads();
     if (sub) A.stamps[8 * f + 4] = __builtin_amdgcn_s_memrealtime();
-    double* L = A.L + A.L_off[f];
-    if (NT == 64 && m <= 64) {
+    double* L = Lf;
+    if (!lds_L) {
+        // every column was written by the register path
+    } else if (NT == 64 && m <= 64) {
         // one wave, m <= 64: column j is one coalesced store, lane = row offset from the diagonal.
         // Per-column data lives in lane j and is broadcast with readlane (scalar, uniform control).
         const int mykind = tid < p ? (int)piv[tid] : 0;
@@ -707,7 +807,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             for (int u = 0; u < 4; ++u) {
                 const int j = j0 + u;
                 if (j < p) {  // uniform
-                    if (j + tid < m) L[cs + tid] = v[u];
+                    if (j + tid < m && !((fastmask >> j) & 1)) L[cs + tid] = v[u];
                     cs += m - j;
                 }
             }
@@ -744,7 +844,23 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     if (sub) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
     // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
     const int cm = m - p;
-    if (cm > 0) {
+    if constexpr (REG && W == 1) {
+        // contribution block straight from the registers: element (i, j), p <= j <= i < m
+        if (cm > 0) {
+            double* cb = A.cb + A.cb_off[f];
+            const int ty = tid / G, tx = tid % G;
+#pragma unroll
+            for (int a = 0; a < RM; ++a) {
+                const int i = ty + G * a;
+                if (G * (a + 1) <= p) continue;  // uniform: block entirely in the pivot rows
+#pragma unroll
+                for (int b = 0; b <= a; ++b) {
+                    const int j = tx + G * b;
+                    if (i < m && j >= p && j <= i) cb[((i - p) * (i - p + 1)) / 2 + (j - p)] = R[a][b];
+                }
+            }
+        }
+    } else if (cm > 0) {
         double* cb = A.cb + A.cb_off[f];
         const int ctot = cm * (cm + 1) / 2;
         constexpr int WB = 4;  // batch: all LDS reads, then all stores (one LDS wait per batch)
