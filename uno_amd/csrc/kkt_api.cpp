@@ -270,9 +270,8 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
             if (global) {
                 while (r < e && S.f_m[lv[r]] > kMaxLdsFront) ++r;
             } else {
-                int cap = 16;
-                for (int x : caps) if (x < m0) cap = x;  // largest cap below m0 ...
-                int floor_ = cap < m0 ? cap : 0;         // ... is the class floor
+                int floor_ = 0;  // largest cap below m0 is the class floor
+                for (int x : caps) if (x < m0) floor_ = x;
                 while (true) {
                     while (r < e && S.f_m[lv[r]] > floor_) ++r;
                     if (r >= e || r - q >= kMinClass || floor_ == 0 || kernel_of(S.f_m[lv[r]]) != kernel_of(m0)) break;
