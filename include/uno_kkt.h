@@ -105,6 +105,37 @@ void* uno_kkt_stream(uno_kkt_t handle);
 /* Human-readable description of the last error on this handle ("" if none). */
 const char* uno_kkt_last_error(uno_kkt_t handle);
 
+/* ---- Device-side vector work around the solve ----
+ * For a caller whose iterate lives in HBM: all vector arguments are DEVICE pointers, work is queued
+ * on the solver's stream (uno_kkt_stream).
+ *
+ * Augmented right-hand side, Subproblem::assemble_augmented_rhs (uno/ingredients/subproblem/Subproblem.cpp:80-99):
+ *   rhs[i] = -grad[i] + sum_j y[j] * J[j][i]  (i < n_vars; terms of y[j] == 0 skipped, constraint-ascending
+ *   order as the reference), rhs[n_vars + j] = -cons[j].  uno_kkt_rhs_setup takes the Jacobian pattern once
+ *   (host arrays: entry e is d cons[jac_con[e]] / d x[jac_var[e]]); jac_values are in that entry order. */
+int uno_kkt_rhs_setup(uno_kkt_t handle, int64_t n_vars, int64_t n_cons, int64_t nnz_jac, const int64_t* jac_con,
+                      const int64_t* jac_var);
+int uno_kkt_assemble_rhs(uno_kkt_t handle, const double* grad, const double* cons, const double* y,
+                         const double* jac_values, double* rhs);
+
+/* Primal-dual direction, PrimalDualInteriorPointProblem::assemble_primal_dual_direction
+ * (PrimalDualInteriorPointProblem.cpp:173-194) with compute_bound_dual_direction (:262-278) and the
+ * fraction-to-boundary rules (:281-325), tau = max(tau_min, 1 - barrier_parameter): dx = sol[0:n],
+ * dy = -sol[n:n+m], bound-dual directions for variables with finite lb / ub (+-inf = unbounded), then
+ * dx, dy scaled by the primal step length and dzl, dzu by the dual one.  step_lengths (HOST, 2 doubles)
+ * receives {primal, dual}. */
+int uno_kkt_assemble_direction(uno_kkt_t handle, int64_t n_vars, int64_t n_cons, const double* solution,
+                               const double* x, const double* lb, const double* ub, const double* zl, const double* zu,
+                               double barrier_parameter, double tau_min, double* dx, double* dy, double* dzl,
+                               double* dzu, double* step_lengths);
+
+/* y += A x with the analysed pattern and the values of the last factorization / value edit,
+ * SymmetricMatrix::product (uno/linear_algebra/SymmetricMatrix.hpp:100-109); vectors in original numbering.
+ * uno_kkt_quadratic_product: x^T A y into *result (HOST), SymmetricMatrix::quadratic_product (:112-130).
+ * One-GPU handles only. */
+int uno_kkt_symv(uno_kkt_t handle, const double* x, double* y);
+int uno_kkt_quadratic_product(uno_kkt_t handle, const double* x, const double* y, double* result);
+
 /* ---- Multi-GPU: one factorization partitioned over the GPUs of a node ----
  * The assembly tree is cut into independent subtrees, one set per rank, factored without any
  * communication; the subtree roots' contribution blocks go to rank 0 (RCCL point-to-point over xGMI),

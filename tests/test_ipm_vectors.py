@@ -1,0 +1,141 @@
+"""Device-side vector work around the KKT solve against the CPU oracle
+(oracle/ipm_oracle.py, a restatement of the reference loops in their floating-point order).
+
+Bars: the right-hand side and the direction (with both step lengths) are bit-identical to the oracle
+(same operation order, no FMA contraction); symv / quadratic_product differ from the reference's COO
+order only by summation order: relative error <= 1e-13 (symv, per entry against the row's |A| |x|
+sum) and 1e-12 (quadratic product)."""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+import ipm_oracle  # noqa: E402
+
+
+def random_ipm_point(rng, n, m, nnz_per_con=8):
+    jc = np.repeat(np.arange(m), nnz_per_con)
+    jv = rng.integers(0, n, size=m * nnz_per_con)
+    perm = rng.permutation(len(jc))          # entries in arbitrary stored order
+    jc, jv = jc[perm], jv[perm]
+    jval = rng.uniform(-2, 2, size=len(jc))
+    grad = rng.standard_normal(n)
+    cons = rng.standard_normal(m)
+    y = rng.standard_normal(m)
+    y[rng.random(m) < 0.2] = 0.0             # zero multipliers are skipped by the reference
+    return grad, cons, y, jc, jv, jval
+
+
+def test_oracle_rhs_matches_dense():
+    rng = np.random.default_rng(1)
+    n, m = 60, 25
+    grad, cons, y, jc, jv, jval = random_ipm_point(rng, n, m)
+    J = np.zeros((m, n))
+    np.add.at(J, (jc, jv), jval)
+    rhs = ipm_oracle.assemble_augmented_rhs(grad, cons, y, jc, jv, jval)
+    np.testing.assert_allclose(rhs[:n], -grad + J.T @ y, rtol=1e-13, atol=1e-13)
+    np.testing.assert_array_equal(rhs[n:], -cons)
+
+
+def test_oracle_direction_small():
+    # one lower-bounded, one upper-bounded, one free variable, one constraint
+    sol = np.array([-1.0, 2.0, 5.0, 3.0])
+    x = np.array([1.0, 0.0, 0.0])
+    lb = np.array([0.0, -np.inf, -np.inf])
+    ub = np.array([np.inf, 1.0, np.inf])
+    zl = np.array([0.5, 0.0, 0.0])
+    zu = np.array([0.0, 0.25, 0.0])
+    dx, dy, dzl, dzu, (ap, ad) = ipm_oracle.assemble_direction(sol, x, lb, ub, zl, zu, 0.1, 0.99)
+    tau = 0.99
+    ap_ref = min(1.0, -tau * 1.0 / -1.0, -tau * (0.0 - 1.0) / 2.0)
+    assert ap == pytest.approx(ap_ref)
+    assert dy[0] == pytest.approx(-3.0 * ap)
+    dzl0 = (0.1 - (-1.0) * 0.5) / 1.0 - 0.5
+    assert dzl[0] == pytest.approx(dzl0 * ad)
+
+
+def test_oracle_symv_matches_dense():
+    rng = np.random.default_rng(2)
+    n = 30
+    r = rng.integers(0, n, 120)
+    c = rng.integers(0, n, 120)
+    v = rng.standard_normal(120)
+    A = np.zeros((n, n))
+    for a, b, w in zip(r, c, v):
+        A[a, b] += w
+        if a != b:
+            A[b, a] += w
+    x, yv = rng.standard_normal(n), rng.standard_normal(n)
+    np.testing.assert_allclose(ipm_oracle.symv(n, r, c, v, x), A @ x, rtol=1e-12, atol=1e-12)
+    assert ipm_oracle.quadratic_product(r, c, v, x, yv) == pytest.approx(x @ A @ yv, rel=1e-12)
+
+
+@pytest.mark.gpu
+def test_device_rhs_and_direction_bitwise():
+    import torch
+    import uno_amd
+    rng = np.random.default_rng(3)
+    n, m = 20000, 7000
+    grad, cons, y, jc, jv, jval = random_ipm_point(rng, n, m)
+    g = uno_amd.HipKKT(0)
+    g.rhs_setup(n, m, jc, jv)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    G, C, Y, JV = d(grad), d(cons), d(y), d(jval)
+    rhs = torch.empty(n + m, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()  # torch's copies run on its own stream; the solver has its own
+    g.assemble_rhs(G.data_ptr(), C.data_ptr(), Y.data_ptr(), JV.data_ptr(), rhs.data_ptr())
+    torch.cuda.synchronize()
+    ref = ipm_oracle.assemble_augmented_rhs(grad, cons, y, jc, jv, jval)
+    np.testing.assert_array_equal(rhs.cpu().numpy(), ref)
+
+    sol = rng.standard_normal(n + m)
+    x = rng.uniform(-1, 1, n)
+    lb = np.where(rng.random(n) < 0.6, x - rng.uniform(0.01, 2, n), -np.inf)
+    ub = np.where(rng.random(n) < 0.4, x + rng.uniform(0.01, 2, n), np.inf)
+    zl = np.where(np.isfinite(lb), rng.uniform(0.01, 1, n), 0.0)
+    zu = np.where(np.isfinite(ub), rng.uniform(0.01, 1, n), 0.0)
+    out = [torch.empty(k, dtype=torch.float64, device="cuda") for k in (n, m, n, n)]
+    ins = [d(a) for a in (sol, x, lb, ub, zl, zu)]  # kept alive across the call
+    torch.cuda.synchronize()
+    steps = g.assemble_direction(n, m, *[t.data_ptr() for t in ins], 1e-3, 0.99, *[o.data_ptr() for o in out])
+    dx, dy, dzl, dzu, (ap, ad) = ipm_oracle.assemble_direction(sol, x, lb, ub, zl, zu, 1e-3, 0.99)
+    assert steps == (ap, ad) and 0.0 < ap <= 1.0 and 0.0 < ad <= 1.0
+    for got, want in zip(out, (dx, dy, dzl, dzu)):
+        np.testing.assert_array_equal(got.cpu().numpy(), want)
+
+
+@pytest.mark.gpu
+def test_device_symv_and_quadratic_product():
+    import torch
+    import uno_amd
+    n, nv, m, r, c, v, b = uno_amd.arrowband(3000, uno_amd.SEEDS["C2"])
+    g = uno_amd.HipKKT(0)
+    g.analyze(n, r, c)
+    g.factorize(v)
+    g.inertia()
+    rng = np.random.default_rng(4)
+    x, w = rng.standard_normal(n), rng.standard_normal(n)
+    X = torch.from_numpy(x).cuda()
+    W = torch.from_numpy(w).cuda()
+    Y = torch.from_numpy(w.copy()).cuda()     # y += A x on top of w
+    torch.cuda.synchronize()
+    g.symv(X.data_ptr(), Y.data_ptr())
+    torch.cuda.synchronize()
+    ref = w + ipm_oracle.symv(n, r, c, v, x)
+    scale = ipm_oracle.symv(n, r, c, np.abs(v), np.abs(x)) + np.abs(w)
+    assert (np.abs(Y.cpu().numpy() - ref) <= 1e-13 * scale + 1e-300).all()
+    q = g.quadratic_product(W.data_ptr(), X.data_ptr())
+    qref = ipm_oracle.quadratic_product(r, c, v, w, x)
+    assert abs(q - qref) <= 1e-12 * abs(np.abs(w) @ ipm_oracle.symv(n, r, c, np.abs(v), np.abs(x)))
+    # values edited on the device are picked up (the packed copy is refreshed)
+    g.fill_values(0, nv, 2.0)
+    Y.zero_()
+    torch.cuda.synchronize()
+    g.symv(X.data_ptr(), Y.data_ptr())
+    v2 = v.copy()
+    v2[:nv] = 2.0
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(Y.cpu().numpy(), ipm_oracle.symv(n, r, c, v2, x), rtol=1e-12, atol=1e-12)

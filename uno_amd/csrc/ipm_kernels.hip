@@ -1,0 +1,199 @@
+// ipm_kernels.hip -- device-side vector work around the KKT solve of Uno's ipopt preset (SURVEY.md 8(a)
+// rows A10, A11, A15), so an iterate that lives in HBM never round-trips to the host:
+//   k_rhs_*      Subproblem::assemble_augmented_rhs            (uno/ingredients/subproblem/Subproblem.cpp:80-99)
+//   k_direction  PrimalDualInteriorPointProblem::assemble_primal_dual_direction + compute_bound_dual_direction
+//                + primal/dual_fraction_to_boundary  (PrimalDualInteriorPointProblem.cpp:173-194, 262-325)
+//   k_symv       SymmetricMatrix::product / quadratic_product  (uno/linear_algebra/SymmetricMatrix.hpp:100-130)
+// All HBM-bound streaming kernels: grid-stride loops, coalesced loads, no same-address atomics except one
+// per workgroup for the step-length minima.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdint>
+
+#include "ipm_kernels.hpp"
+
+// no FMA contraction: the reference's host arithmetic (g++, x86-64 baseline) rounds every product and
+// sum separately, and the right-hand side and the direction are compared bit for bit with it
+#pragma clang fp contract(off)
+
+namespace ukkt {
+
+namespace {
+constexpr int kT = 256;
+
+int grid_of(int64_t n) {
+    int64_t g = (n + kT - 1) / kT;
+    return (int)(g < 1 ? 1 : (g > 8192 ? 8192 : g));
+}
+
+__device__ __forceinline__ unsigned long long bits(double d) { return (unsigned long long)__double_as_longlong(d); }
+}  // namespace
+
+// rhs[i] = -g[i] + sum_{e in column i of J^T, ascending constraint} y[c_e] * d_e  (i < n)
+// rhs[n + j] = -c[j].  The per-variable entry lists are sorted by constraint index, the order in which
+// the reference accumulates (it loops constraints in order), so the sums are bit-identical; entries
+// of constraints with y_j == 0 are skipped as in the reference (Subproblem.cpp:89).
+__global__ void k_rhs(const double* __restrict__ grad, const double* __restrict__ cons, const double* __restrict__ y,
+                      const double* __restrict__ jval, const int64_t* __restrict__ vptr, const int32_t* __restrict__ vent,
+                      const int32_t* __restrict__ jcon, int64_t n, int64_t m, double* __restrict__ rhs) {
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n + m; i += (int64_t)gridDim.x * kT) {
+        if (i < n) {
+            double r = -grad[i];
+            for (int64_t q = vptr[i]; q < vptr[i + 1]; ++q) {
+                const int32_t e = vent[q];
+                const double yj = y[jcon[e]];
+                if (yj != 0.0) r += yj * jval[e];
+            }
+            rhs[i] = r;
+        } else {
+            rhs[i] = -cons[i - n];
+        }
+    }
+}
+
+// direction + fraction-to-boundary step lengths; alpha[0] / alpha[1] hold the bit patterns of the
+// primal / dual step lengths (positive doubles order like their bits: one atomicMin per workgroup)
+__global__ void k_direction(DirArgs A) {
+    __shared__ unsigned long long red[2][kT / 64];
+    double ap = 1.0, ad = 1.0;
+    const int64_t n = A.n;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n + A.m; i += (int64_t)gridDim.x * kT) {
+        if (i >= n) {  // constraint multipliers: dy = -solution (PrimalDualInteriorPointProblem.cpp:178)
+            A.dy[i - n] = -A.sol[i];
+            continue;
+        }
+        const double dx = A.sol[i];
+        const double x = A.x[i];
+        A.dx[i] = dx;
+        double dzl = 0.0, dzu = 0.0;
+        const double lb = A.lb[i], ub = A.ub[i];
+        if (isfinite(lb)) {  // lower-bounded variable (:266-271, :285-291, :307-313)
+            const double zl = A.zl[i];
+            const double dist = x - lb;
+            dzl = (A.mu - dx * zl) / dist - zl;
+            if (dx < 0.0) {
+                const double d = -A.tau * dist / dx;
+                if (0.0 < d) ap = fmin(ap, d);
+            }
+            if (dzl < 0.0) {
+                const double d = -A.tau * zl / dzl;
+                if (0.0 < d) ad = fmin(ad, d);
+            }
+        }
+        if (isfinite(ub)) {  // upper-bounded variable (:272-277, :292-299, :314-320)
+            const double zu = A.zu[i];
+            const double dist = x - ub;
+            dzu = (A.mu - dx * zu) / dist - zu;
+            if (0.0 < dx) {
+                const double d = -A.tau * dist / dx;
+                if (0.0 < d) ap = fmin(ap, d);
+            }
+            if (0.0 < dzu) {
+                const double d = -A.tau * zu / dzu;
+                if (0.0 < d) ad = fmin(ad, d);
+            }
+        }
+        A.dzl[i] = dzl;
+        A.dzu[i] = dzu;
+    }
+    unsigned long long bp = bits(ap), bd = bits(ad);
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned long long op = __shfl_xor(bp, off), od = __shfl_xor(bd, off);
+        bp = op < bp ? op : bp;
+        bd = od < bd ? od : bd;
+    }
+    if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = bp; red[1][threadIdx.x >> 6] = bd; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kT / 64; ++w) {
+            bp = red[0][w] < bp ? red[0][w] : bp;
+            bd = red[1][w] < bd ? red[1][w] : bd;
+        }
+        atomicMin(A.alpha, bp);
+        atomicMin(A.alpha + 1, bd);
+    }
+}
+
+// scaling by the step lengths (PrimalDualInteriorPointProblem.cpp:190-193)
+__global__ void k_direction_scale(DirArgs A) {
+    const double ap = __longlong_as_double((long long)A.alpha[0]);
+    const double ad = __longlong_as_double((long long)A.alpha[1]);
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < A.n + A.m; i += (int64_t)gridDim.x * kT) {
+        if (i < A.n) {
+            A.dx[i] *= ap;
+            A.dzl[i] *= ad;
+            A.dzu[i] *= ad;
+        } else {
+            A.dy[i - A.n] *= ap;
+        }
+    }
+}
+
+// y += A x for the symmetric matrix held as unique lower-triangle slots, row by row (atomic-free):
+// row i = its column part (slots cptr[i] .. cptr[i+1], partner = later row) + its row part (rslot)
+__global__ void k_symv(SymvArgs A) {
+    const int64_t g = ((int64_t)blockIdx.x * kT + threadIdx.x) / 16;
+    const int lane = threadIdx.x & 15;
+    if (g >= A.n) return;
+    const int32_t i = (int32_t)g;
+    const int32_t oi = A.perm[i];
+    double acc = 0.0;
+    for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += 16) acc += A.uval[q] * A.x[A.ent_r[q]];
+    for (int32_t t = A.rptr[i] + lane; t < A.rptr[i + 1]; t += 16) {
+        const int32_t q = A.rslot[t];
+        acc += A.uval[q] * A.x[A.ent_c[q]];
+    }
+    for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
+    if (lane == 0) {
+        A.y[oi] += acc;
+        if (A.dot_w) A.dot_part[i] = A.dot_w[oi] * acc;
+    }
+}
+
+// sum of per-row partials (quadratic_product): one block-sum per workgroup, atomics on one double
+__global__ void k_sum(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
+    __shared__ double red[kT / 64];
+    double s = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) s += v[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kT / 64; ++w) s += red[w];
+        atomicAdd(out, s);
+    }
+}
+
+hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
+                      const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s) {
+    if (n + m == 0) return hipSuccess;
+    hipLaunchKernelGGL(k_rhs, dim3(grid_of(n + m)), dim3(kT), 0, s, grad, cons, y, jval, vptr, vent, jcon, n, m, rhs);
+    return hipGetLastError();
+}
+
+__global__ void k_alpha_init(unsigned long long* alpha) {
+    if (threadIdx.x < 2) alpha[threadIdx.x] = 0x3ff0000000000000ull;  // 1.0
+}
+
+hipError_t launch_direction(const DirArgs& A, hipStream_t s) {
+    hipLaunchKernelGGL(k_alpha_init, dim3(1), dim3(64), 0, s, A.alpha);
+    if (A.n + A.m == 0) return hipGetLastError();
+    hipLaunchKernelGGL(k_direction, dim3(grid_of(A.n + A.m)), dim3(kT), 0, s, A);
+    hipLaunchKernelGGL(k_direction_scale, dim3(grid_of(A.n + A.m)), dim3(kT), 0, s, A);
+    return hipGetLastError();
+}
+
+hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s) {
+    if (A.n == 0) return hipSuccess;
+    const int64_t threads = A.n * 16;
+    hipLaunchKernelGGL(k_symv, dim3((unsigned)((threads + kT - 1) / kT)), dim3(kT), 0, s, A);
+    if (A.dot_w) {
+        hipError_t e = hipMemsetAsync(dot_out, 0, sizeof(double), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_sum, dim3(grid_of(A.n) > 1024 ? 1024 : grid_of(A.n)), dim3(kT), 0, s, A.dot_part, A.n, dot_out);
+    }
+    return hipGetLastError();
+}
+
+}  // namespace ukkt

@@ -1,0 +1,46 @@
+// ipm_kernels.hpp -- device vector kernels around the KKT solve (ipm_kernels.hip).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace ukkt {
+
+struct DirArgs {
+    int64_t n, m;
+    const double* sol;  // KKT solution, n + m
+    const double* x;    // current primals
+    const double* lb;   // variable bounds (+-inf = unbounded)
+    const double* ub;
+    const double* zl;   // bound multipliers
+    const double* zu;
+    double mu, tau;
+    double* dx;
+    double* dy;
+    double* dzl;
+    double* dzu;
+    unsigned long long* alpha;  // [primal, dual] step length bits (device)
+};
+
+struct SymvArgs {
+    int64_t n;
+    const int32_t* perm;
+    const int32_t* cptr;
+    const int32_t* rptr;
+    const int32_t* rslot;
+    const int32_t* ent_r;
+    const int32_t* ent_c;
+    const double* uval;
+    const double* x;      // by original index
+    double* y;            // y += A x, by original index
+    const double* dot_w;  // optional: w^T A x partials (quadratic_product), by original index
+    double* dot_part;     // per row (new numbering)
+};
+
+hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
+                      const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s);
+hipError_t launch_direction(const DirArgs& A, hipStream_t s);
+hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s);
+
+}  // namespace ukkt

@@ -17,6 +17,7 @@
 #include "../../include/uno_kkt_debug.h"
 #include "analysis.hpp"
 #include "comm.hpp"
+#include "ipm_kernels.hpp"
 #include "kkt_kernels.hpp"
 
 using namespace ukkt;
@@ -46,8 +47,8 @@ struct DBuf {
     ~DBuf() { release(); }
 };
 
-enum KernelClass { KC_PACK = 0, KC_SCALE, KC_FACTOR_LDS, KC_FACTOR_GLOBAL, KC_SOLVE_FWD, KC_SOLVE_BWD, KC_RHS, KC_COUNT };
-const char* kClassNames[KC_COUNT] = {"pack", "scale", "factor_lds", "factor_global", "solve_fwd", "solve_bwd", "rhs"};
+enum KernelClass { KC_PACK = 0, KC_SCALE, KC_FACTOR_LDS, KC_FACTOR_GLOBAL, KC_SOLVE_FWD, KC_SOLVE_BWD, KC_RHS, KC_SYMV, KC_COUNT };
+const char* kClassNames[KC_COUNT] = {"pack", "scale", "factor_lds", "factor_global", "solve_fwd", "solve_bwd", "rhs", "symv"};
 
 struct Launch {
     int begin, count, mmax;
@@ -121,6 +122,13 @@ struct uno_kkt {
     unsigned long long* h_counters = nullptr;
     Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
     // distributed factorization (null comm: one GPU)
+    // device-side vector work around the solve
+    int64_t rhs_n = -1, rhs_m = -1;
+    DBuf<int64_t> jv_ptr;                 // per variable: range into jv_ent (Jacobian entries, constraint-ascending)
+    DBuf<int32_t> jv_ent, j_con;
+    DBuf<unsigned long long> alpha;
+    DBuf<double> symv_tmp, symv_part, dot_d;
+    bool packed_valid = false;            // uval holds the current values (symv reuses the factor's pack)
     ukkt::Transport* comm = nullptr;
     int rank = 0, world = 1;
     int gather_solution = 1;
@@ -805,6 +813,7 @@ int uno_kkt_set_values(uno_kkt_t h, const int64_t* positions, const double* v, i
     if (!h->analyzed || !h->values_ptr) return set_err(h, UNO_KKT_ERR_STATE, "set_values before a factorization");
     if (count < 0 || (count > 0 && (!positions || !v))) return set_err(h, UNO_KKT_ERR_ARG, "bad arguments");
     HIPCHK(h, hipSetDevice(h->device));
+    h->packed_valid = false;
     // small host-driven edit: positions are few (regularization diagonal), copy one by one in batches
     for (int64_t i = 0; i < count; ++i) {
         if (positions[i] < 0 || positions[i] >= h->S.nnz) return set_err(h, UNO_KKT_ERR_ARG, "position out of range");
@@ -829,6 +838,7 @@ int uno_kkt_fill_values(uno_kkt_t h, int64_t first, int64_t count, double value)
     if (first < 0 || count < 0 || first + count > h->S.nnz) return set_err(h, UNO_KKT_ERR_ARG, "range out of bounds");
     if (count == 0) return UNO_KKT_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    h->packed_valid = false;
     int grid = (int)std::min<int64_t>((count + 255) / 256, 4096);
     hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, h->stream, const_cast<double*>(h->values_ptr) + first, count, value);
     HIPCHK(h, hipGetLastError());
@@ -856,6 +866,7 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     }
     int rc = enqueue_factorization(h);
     if (rc != UNO_KKT_OK) return rc;
+    h->packed_valid = h->world == 1;  // one GPU packs every slot
     h->st.factorizations++;
     return UNO_KKT_OK;
 }
@@ -1032,6 +1043,116 @@ int64_t uno_kkt_debug_stamps(uno_kkt_t h, uint64_t* out, int64_t cap, int32_t* f
 }
 
 const char* uno_kkt_last_error(uno_kkt_t h) { return h ? h->err.c_str() : "null handle"; }
+
+// ---- device-side vector work around the solve ----
+int uno_kkt_rhs_setup(uno_kkt_t h, int64_t n_vars, int64_t n_cons, int64_t nnz_jac, const int64_t* jac_con,
+                      const int64_t* jac_var) {
+    if (!h || n_vars < 0 || n_cons < 0 || nnz_jac < 0 || (nnz_jac > 0 && (!jac_con || !jac_var))) return UNO_KKT_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    std::vector<int64_t> ptr(n_vars + 1, 0);
+    std::vector<int32_t> con(nnz_jac);
+    for (int64_t e = 0; e < nnz_jac; ++e) {
+        if (jac_con[e] < 0 || jac_con[e] >= n_cons || jac_var[e] < 0 || jac_var[e] >= n_vars)
+            return set_err(h, UNO_KKT_ERR_ARG, "Jacobian index out of range");
+        ptr[jac_var[e] + 1]++;
+        con[e] = (int32_t)jac_con[e];
+    }
+    for (int64_t i = 0; i < n_vars; ++i) ptr[i + 1] += ptr[i];
+    // per variable, entries in ascending (constraint, position): the reference's accumulation order
+    std::vector<int32_t> ent(nnz_jac);
+    {
+        std::vector<int64_t> fill(ptr.begin(), ptr.end() - 1);
+        std::vector<int32_t> order(nnz_jac);
+        for (int64_t e = 0; e < nnz_jac; ++e) order[e] = (int32_t)e;
+        std::stable_sort(order.begin(), order.end(), [&](int32_t a, int32_t b) { return jac_con[a] < jac_con[b]; });
+        for (int32_t e : order) ent[fill[jac_var[e]]++] = e;
+    }
+    hipStream_t s = h->stream;
+    HIPCHK(h, h->jv_ptr.upload(ptr, s));
+    HIPCHK(h, h->jv_ent.upload(ent, s));
+    HIPCHK(h, h->j_con.upload(con, s));
+    HIPCHK(h, hipStreamSynchronize(s));
+    h->rhs_n = n_vars;
+    h->rhs_m = n_cons;
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_assemble_rhs(uno_kkt_t h, const double* grad, const double* cons, const double* y, const double* jac_values,
+                         double* rhs) {
+    if (!h || !rhs) return UNO_KKT_ERR_ARG;
+    if (h->rhs_n < 0) return set_err(h, UNO_KKT_ERR_STATE, "assemble_rhs before rhs_setup");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, launch_rhs(grad, cons, y, jac_values, h->jv_ptr.p, h->jv_ent.p, h->j_con.p, h->rhs_n, h->rhs_m, rhs,
+                         h->stream));
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_assemble_direction(uno_kkt_t h, int64_t n_vars, int64_t n_cons, const double* solution, const double* x,
+                               const double* lb, const double* ub, const double* zl, const double* zu,
+                               double barrier_parameter, double tau_min, double* dx, double* dy, double* dzl,
+                               double* dzu, double* step_lengths) {
+    if (!h || n_vars < 0 || n_cons < 0 || !step_lengths) return UNO_KKT_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!h->alpha.p) HIPCHK(h, h->alpha.alloc(2));
+    DirArgs A;
+    A.n = n_vars; A.m = n_cons; A.sol = solution; A.x = x; A.lb = lb; A.ub = ub; A.zl = zl; A.zu = zu;
+    A.mu = barrier_parameter;
+    A.tau = std::max(tau_min, 1.0 - barrier_parameter);  // PrimalDualInteriorPointProblem.cpp:183
+    A.dx = dx; A.dy = dy; A.dzl = dzl; A.dzu = dzu; A.alpha = h->alpha.p;
+    HIPCHK(h, launch_direction(A, h->stream));
+    unsigned long long b[2];
+    HIPCHK(h, hipMemcpyAsync(b, h->alpha.p, sizeof(b), hipMemcpyDeviceToHost, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    memcpy(step_lengths, b, sizeof(b));
+    return UNO_KKT_OK;
+}
+
+static int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* dot) {
+    if (!h->analyzed || !h->values_ptr) return set_err(h, UNO_KKT_ERR_STATE, "symv needs analysed pattern and values");
+    if (h->world > 1) return set_err(h, UNO_KKT_ERR_STATE, "symv on a distributed handle");
+    Symbolic& S = h->S;
+    hipStream_t s = h->stream;
+    if (h->factor_enqueued) {
+        int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK) return rc;
+    }
+    if (!h->packed_valid) {
+        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, 0, S.nu, h->uval.p, s));
+        h->packed_valid = true;
+    }
+    SymvArgs A;
+    A.n = S.n; A.perm = h->perm_d.p; A.cptr = h->cptr.p; A.rptr = h->rptr.p; A.rslot = h->rslot.p;
+    A.ent_r = h->ent_r.p; A.ent_c = h->ent_c.p; A.uval = h->uval.p; A.x = x; A.y = y; A.dot_w = w;
+    A.dot_part = nullptr;
+    if (w) {
+        if (h->symv_part.n != (size_t)S.n) HIPCHK(h, h->symv_part.alloc(std::max<int64_t>(S.n, 1)));
+        if (!h->dot_d.p) HIPCHK(h, h->dot_d.alloc(1));
+        A.dot_part = h->symv_part.p;
+    }
+    {
+        TimerScope t(h, KC_SYMV);
+        HIPCHK(h, launch_symv(A, h->dot_d.p, s));
+    }
+    if (w) {
+        HIPCHK(h, hipMemcpyAsync(dot, h->dot_d.p, sizeof(double), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+    }
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_symv(uno_kkt_t h, const double* x, double* y) {
+    if (!h || !x || !y) return UNO_KKT_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    return symv_impl(h, x, y, nullptr, nullptr);
+}
+
+int uno_kkt_quadratic_product(uno_kkt_t h, const double* x, const double* y, double* result) {
+    if (!h || !x || !y || !result) return UNO_KKT_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->symv_tmp.n != (size_t)h->S.n) HIPCHK(h, h->symv_tmp.alloc(std::max<int64_t>(h->S.n, 1)));
+    if (h->S.n > 0) HIPCHK(h, hipMemsetAsync(h->symv_tmp.p, 0, sizeof(double) * h->S.n, h->stream));
+    return symv_impl(h, y, h->symv_tmp.p, x, result);  // x^T (A y)
+}
 
 // ---- distributed factorization ----
 int uno_kkt_comm_unique_id(unsigned char id[128]) {

@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = [
     "uno_kkt_set_values", "uno_kkt_fill_values", "uno_kkt_inertia", "uno_kkt_solve", "uno_kkt_stats",
     "uno_kkt_kernel_times", "uno_kkt_reset_kernel_times", "uno_kkt_stream", "uno_kkt_last_error",
     "uno_kkt_version", "uno_kkt_comm_unique_id", "uno_kkt_attach_rccl", "uno_kkt_group_create",
-    "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info",
+    "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info", "uno_kkt_rhs_setup",
+    "uno_kkt_assemble_rhs", "uno_kkt_assemble_direction", "uno_kkt_symv", "uno_kkt_quadratic_product",
 ]
 
 
@@ -98,6 +99,12 @@ def load_library():
     lib.uno_kkt_debug_partition.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _i64p]
     lib.uno_kkt_debug_partition.restype = ctypes.c_int64
+    lib.uno_kkt_rhs_setup.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p]
+    lib.uno_kkt_assemble_rhs.argtypes = [vp, vp, vp, vp, vp, vp]
+    lib.uno_kkt_assemble_direction.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
+                                               ctypes.c_double, ctypes.c_double, vp, vp, vp, vp, _f64p]
+    lib.uno_kkt_symv.argtypes = [vp, vp, vp]
+    lib.uno_kkt_quadratic_product.argtypes = [vp, vp, vp, _f64p]
     _lib = lib
     return lib
 
@@ -207,6 +214,33 @@ class HipKKT:
 
     def reset_kernel_times(self):
         self._check(self.lib.uno_kkt_reset_kernel_times(self.h))
+
+    # ---- device-side vector work (A10, A11, A15); vector arguments are device addresses (int) ----
+    def rhs_setup(self, n_vars, n_cons, jac_con, jac_var):
+        c, cp = _i64(jac_con)
+        v, vpp = _i64(jac_var)
+        self._check(self.lib.uno_kkt_rhs_setup(self.h, int(n_vars), int(n_cons), len(c), cp, vpp))
+
+    def assemble_rhs(self, grad, cons, y, jac_values, rhs):
+        P = lambda a: ctypes.c_void_p(int(a))
+        self._check(self.lib.uno_kkt_assemble_rhs(self.h, P(grad), P(cons), P(y), P(jac_values), P(rhs)))
+
+    def assemble_direction(self, n_vars, n_cons, solution, x, lb, ub, zl, zu, mu, tau_min, dx, dy, dzl, dzu):
+        P = lambda a: ctypes.c_void_p(int(a))
+        steps = np.zeros(2)
+        self._check(self.lib.uno_kkt_assemble_direction(self.h, int(n_vars), int(n_cons), P(solution), P(x), P(lb), P(ub),
+                                                        P(zl), P(zu), float(mu), float(tau_min), P(dx), P(dy), P(dzl),
+                                                        P(dzu), steps.ctypes.data_as(_f64p)))
+        return float(steps[0]), float(steps[1])
+
+    def symv(self, x_ptr, y_ptr):
+        self._check(self.lib.uno_kkt_symv(self.h, ctypes.c_void_p(int(x_ptr)), ctypes.c_void_p(int(y_ptr))))
+
+    def quadratic_product(self, x_ptr, y_ptr):
+        r = ctypes.c_double()
+        self._check(self.lib.uno_kkt_quadratic_product(self.h, ctypes.c_void_p(int(x_ptr)), ctypes.c_void_p(int(y_ptr)),
+                                                       ctypes.byref(r)))
+        return r.value
 
     # ---- multi-GPU (one factorization partitioned over ranks; attach before analyze) ----
     def attach_rccl(self, unique_id, rank, world):
