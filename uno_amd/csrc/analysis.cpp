@@ -479,12 +479,16 @@ int64_t delay_columns(Pattern& P, const Symbolic& S, const std::vector<int32_t>&
     std::vector<char> moved(P.n, 0);
     std::vector<std::vector<int32_t>> into(nf);  // new indices delayed into each block
     int64_t count = 0;
+    if ((int64_t)P.delay_count.size() != P.n) P.delay_count.assign(P.n, 0);
     for (int32_t v : delayed_vars) {
         if (v < 0 || v >= P.n) continue;
         int32_t j = iperm[v];
         if (moved[j]) continue;
         int32_t par = S.f_parent[blk[j]];
         if (par < 0) continue;  // roots cannot delay
+        if (P.delay_count[v] < 255) P.delay_count[v]++;
+        if (P.delay_count[v] >= 2)  // failed again after a delay: the cascade would climb level by level
+            while (S.f_parent[par] >= 0) par = S.f_parent[par];
         moved[j] = 1;
         into[par].push_back(j);
         count++;

@@ -32,6 +32,7 @@ struct Pattern {
     std::vector<int32_t> ai;
     std::vector<int32_t> perm;              // nested-dissection order (new -> original)
     std::vector<int32_t> bfirst;            // supernode boundaries in the new order (nb+1)
+    std::vector<uint8_t> delay_count;       // per original variable: times its pivot was delayed
     int64_t n_dense = 0;
 };
 
@@ -79,7 +80,9 @@ std::string build_structure(const Pattern& P, Symbolic& S);
 // the parent's, i.e. their pivots are delayed to the parent).  Returns the number merged.
 int64_t amalgamate(Pattern& P, const Symbolic& S, const std::vector<char>& merge);
 // Delayed pivots at column granularity: every listed column (original id) whose front has a parent
-// is moved into its parent's block (eliminated just before the parent's own columns).
+// is moved into its parent's block (eliminated just before the parent's own columns); a column
+// delayed for the second time goes straight to the root of its tree (one rebuild instead of one per
+// level of a cascade).
 int64_t delay_columns(Pattern& P, const Symbolic& S, const std::vector<int32_t>& delayed_vars);
 
 // Subtree partition of the assembly tree over `world` ranks: the top of the tree is

@@ -104,6 +104,7 @@ struct uno_kkt {
     Symbolic S;
     int delay_relaxed = 1;      // also amalgamate fronts whose pivots needed a relaxed threshold (MUMPS: delay)
     int max_merge_rounds = 64;
+    int verbose = 0;
     int64_t merges_total = 0;
     bool analyzed = false, factor_enqueued = false, factored = false;
     const double* values_ptr = nullptr;  // device values used by the last factorization
@@ -517,15 +518,23 @@ int finish_factorization(uno_kkt_t h) {
         }
         if (moved == 0) break;
         h->merges_total += moved;
+        auto tb = std::chrono::steady_clock::now();
         std::string msg = build_structure(h->P, h->S);
         if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
         int rc = upload_structure(h);
         if (rc != UNO_KKT_OK) return rc;
+        auto tu = std::chrono::steady_clock::now();
         rc = enqueue_factorization(h);
         if (rc != UNO_KKT_OK) return rc;
         HIPCHK(h, hipStreamSynchronize(h->stream));
         flush_timing(h);
         h->factor_enqueued = false;
+        if (h->verbose)
+            fprintf(stderr, "[uno_kkt] merge round %d: %lld delayed columns listed, %lld moved, stuck %llu; "
+                            "rebuild %.3f s, upload %.3f s, refactor %.3f s, fronts %lld\n", round, (long long)dv.size(),
+                    (long long)moved, (unsigned long long)c[5],
+                    std::chrono::duration<double>(tu - tb).count() - 0.0,
+                    0.0, std::chrono::duration<double>(std::chrono::steady_clock::now() - tu).count(), (long long)h->S.nf);
     }
     const unsigned long long* c = h->h_counters;
     h->st.pivots_2x2 = (int64_t)c[3];
@@ -781,6 +790,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else if (n == "gather_solution") h->gather_solution = value != 0.0;
+    else if (n == "verbose") h->verbose = (int)value;
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;
 }
