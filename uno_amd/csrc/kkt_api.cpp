@@ -229,7 +229,7 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
                 const int m = S.f_m[f], p = S.f_p[f];
                 if (p <= 64 && m <= kMaxLdsFront) {
                     const int sz = p * m - p * (p - 1) / 2;
-                    wv.push_back({((sz + 1) & ~1) + m, f});
+                    wv.push_back({((sz + 1) & ~1) + ((m + 1) & ~1) + (m + 1) / 2, f});
                 } else {
                     big.push_back(f);
                 }
@@ -911,7 +911,8 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     SolveArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
-    A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p;
+    A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p; A.ch_cm = h->ch_cm.p;
+    A.ch_relmap_off = h->ch_relmap_off.p;
     auto run = [&](const Plan& P, const SolveLaunch& L, bool forward) -> hipError_t {
         const int32_t* fr = P.sol_fronts.p + L.begin;
         return L.wave ? launch_solve_wave(A, fr, L.count, L.lds, forward, s)

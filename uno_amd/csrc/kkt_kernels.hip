@@ -526,7 +526,6 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             // rank-1 update stays in registers; column k itself is left untouched, so L is written
             // from the registers after the loop.
             const int ty = tid / G, tx = tid % G;
-            const int nb = (m + G - 1) / G;  // row blocks holding front rows
             bool need = false;
 #pragma unroll
             for (int bk = 0; bk < RM; ++bk) {
@@ -536,7 +535,6 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     double lv[RM], cv[RM];
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
-                        if (a >= nb) break;  // uniform: row blocks beyond the front
                         lv[a] = bperm_d(R[a][bk], ty * G + kk);  // A(ty + G a, k)
                         cv[a] = bperm_d(R[a][bk], tx * G + kk);  // A(tx + G a, k)
                     }
@@ -545,7 +543,6 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     bool bad = !(aak > thres);
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
-                        if (a >= nb) break;
                         const int i = ty + G * a, j = tx + G * a;
                         lv[a] = (i > k && i < m) ? lv[a] : 0.0;
                         cv[a] = (j > k && j < m) ? cv[a] : 0.0;
@@ -556,16 +553,11 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     if (!need) {  // 1x1 pivot at k without interchange
                         const double dinv = 1.0 / akk;
 #pragma unroll
-                        for (int b = bk; b < RM; ++b) {
-                            if (b >= nb) break;
-                            cv[b] *= dinv;
-                        }
+                        for (int b = bk; b < RM; ++b) cv[b] *= dinv;
 #pragma unroll
-                        for (int a = bk; a < RM; ++a) {
-                            if (a >= nb) break;
+                        for (int a = bk; a < RM; ++a)
 #pragma unroll
                             for (int b = bk; b <= a; ++b) R[a][b] -= lv[a] * cv[b];
-                        }
                         if (tid == 0) { piv[k] = PIV_1X1; if (akk > 0.0) npos++; else nneg++; }
                         fastmask |= 1ull << k;
                         if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; }
@@ -1221,27 +1213,67 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, int64_
 }
 
 __global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* __restrict__ fronts) {
+    // Latency-bound per front: the global loads are grouped into three dependent round trips
+    // {front record} -> {row ids, pivoted positions, pivot kinds, children's edge records, L panel}
+    // -> {w at the pivot rows, children's update vectors and maps (CH children in flight at once)};
+    // everything after that runs from LDS and registers.
     extern __shared__ __attribute__((aligned(16))) double smem_s[];
     const int f = fronts[blockIdx.x];
     const int m = A.fm[f], p = A.fp[f];
     const int lane = threadIdx.x;
     const int64_t ro = A.rows_off[f];
+    const int64_t Lo = A.L_off[f];
+    const int c0 = A.child_off[f], c1 = A.child_off[f + 1];
     const int sz = p * m - p * (p - 1) / 2;
     double* P = smem_s;
     double* y = smem_s + ((sz + 1) & ~1);
+    int32_t* fpl = (int32_t*)(y + ((m + 1) & ~1));  // this front's rows were permuted by pivoting
+    // round trip 2 (m <= kMaxLdsFront = 2 * 64 rows per lane)
     const int mypiv = lane < p ? (int)A.piv[ro + lane] : 0;
-    for (int i = lane; i < m; i += 64) y[i] = i < p ? A.w[A.frow[ro + i]] : 0.0;
-    stage_panel(A.L, A.L_off[f], sz, P);
-    __syncthreads();
-    const int32_t* fpos = A.fpos + ro;  // this front's rows were permuted by pivoting
-    for (int ci = A.child_off[f]; ci < A.child_off[f + 1]; ++ci) {
-        const int c = A.child[ci];
-        const int cm = A.fm[c] - A.fp[c];
-        const int32_t* rm = A.relmap + A.relmap_off[c];
-        const double* cv = A.cvec + A.relmap_off[c];
-        for (int t = lane; t < cm; t += 64) y[fpos[rm[t]]] += cv[t];
-        __syncthreads();
+    int32_t fr0 = 0, fr1 = 0;
+    if (lane < p) fr0 = A.frow[ro + lane];
+    if (lane + 64 < p) fr1 = A.frow[ro + lane + 64];
+    const int32_t fp0 = lane < m ? A.fpos[ro + lane] : 0;
+    const int32_t fp1 = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
+    int my_cm = 0;
+    long long my_rmo = 0;
+    if (lane < c1 - c0) {
+        my_cm = A.ch_cm[c0 + lane];
+        my_rmo = A.ch_relmap_off[c0 + lane];
     }
+    stage_panel(A.L, Lo, sz, P);
+    // round trip 3
+    if (lane < m) { y[lane] = lane < p ? A.w[fr0] : 0.0; fpl[lane] = fp0; }
+    if (lane + 64 < m) { y[lane + 64] = lane + 64 < p ? A.w[fr1] : 0.0; fpl[lane + 64] = fp1; }
+    __syncthreads();
+    constexpr int CH = 4;
+    for (int cb = c0; cb < c1; cb += CH) {
+        if (cb != c0 && (cb - c0) % 64 == 0 && lane < c1 - cb) {  // more than 64 children: next records
+            my_cm = A.ch_cm[cb + lane];
+            my_rmo = A.ch_relmap_off[cb + lane];
+        }
+        double v[CH][2];
+        int32_t r[CH][2];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int q = (cb - c0) % 64 + u;
+            const bool have = cb + u < c1;  // uniform
+            const int cm = have ? __builtin_amdgcn_readlane(my_cm, q) : 0;
+            const int64_t off = have ? (int64_t)readlane64((unsigned long long)my_rmo, q) : 0;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int t = lane + 64 * h;
+                v[u][h] = t < cm ? A.cvec[off + t] : 0.0;
+                r[u][h] = t < cm ? A.relmap[off + t] : -1;
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u)  // children in order (rows of one child are distinct)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                if (r[u][h] >= 0) y[fpl[r[u][h]]] += v[u][h];
+    }
+    __syncthreads();
     // triangle
     double yi = lane < p ? y[lane] : 0.0;
     for (int k = 0; k < p; ++k) {
@@ -1282,7 +1314,7 @@ __global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* 
             const double y0 = y[k0], y1 = y[k0 + 1];
             out = kind == PIV_2X2_A ? (e * y0 - b * y1) / det : (a * y1 - b * y0) / det;
         }
-        A.w[A.frow[ro + lane]] = out;
+        A.w[fr0] = out;
     }
 }
 

@@ -61,6 +61,8 @@ struct SolveArgs {
     const double* L;
     double* w;      // work vector by original id (scaled space)
     double* cvec;   // per-front update vectors (layout of relmap)
+    const int32_t* ch_cm;          // per child edge (aligned with child): update-vector length
+    const int64_t* ch_relmap_off;  // per child edge: offset into relmap / cvec
 };
 
 // row-wise scans for the equilibration and ||A_pre||_inf (kkt_kernels.hip k_rowscan)
@@ -113,7 +115,7 @@ hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 // one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of
-// p*m - p*(p-1)/2 (rounded up to even) + m
+// p*m - p*(p-1)/2 (rounded up to even) + m (rounded up to even) + m / 2 (int32 row positions)
 hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int count, int lds_doubles, bool forward,
                              hipStream_t s);
 // counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
