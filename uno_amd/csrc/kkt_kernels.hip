@@ -520,11 +520,13 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     while (k < p) {
         if constexpr (REG && W == 1) {
-            // One wave owns the whole front (m <= G * RM): column k lives in the lanes with tx = k % G.
-            // Its entries are fetched straight from those lanes' registers with ds_bpermute (one
-            // crossbar round trip, no LDS store, no barrier), the threshold test is one ballot and the
-            // rank-1 update stays in registers; column k itself is left untouched, so L is written
-            // from the registers after the loop.
+            // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of
+            // the lanes with tx = k % G.  Those lanes test it in place (one compare per row block,
+            // one ballot) and publish it to an LDS vector (one store per block) that every lane reads
+            // back as its row / column operands (in-wave LDS ordering: no barrier); the rank-1 update
+            // stays in registers.  Rows <= k of column k are never read back (upper-triangle register
+            // slots are scratch) and column k itself is left untouched, so L is written from the
+            // registers after the loop.
             const int ty = tid / G, tx = tid % G;
             bool need = false;
 #pragma unroll
@@ -532,28 +534,28 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                 while (!need && k < p && k / G == bk) {
                     if (stamping) t_mark = __builtin_amdgcn_s_memtime();
                     const int kk = k - G * bk;
-                    double lv[RM], cv[RM];
-#pragma unroll
-                    for (int a = bk; a < RM; ++a) {
-                        lv[a] = bperm_d(R[a][bk], ty * G + kk);  // A(ty + G a, k)
-                        cv[a] = bperm_d(R[a][bk], tx * G + kk);  // A(tx + G a, k)
-                    }
+                    const bool owner = tx == kk;
                     const double akk = readlane_d(R[bk][bk], kk * G + kk);
                     const double aak = fabs(akk);
-                    bool bad = !(aak > thres);
+                    bool bad = false;
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
-                        const int i = ty + G * a, j = tx + G * a;
-                        lv[a] = (i > k && i < m) ? lv[a] : 0.0;
-                        cv[a] = (j > k && j < m) ? cv[a] : 0.0;
-                        bad |= A.u * fabs(lv[a]) > aak;
+                        const int i = ty + G * a;
+                        if (owner && i < m) colv[i] = R[a][bk];  // colv has m entries
+                        bad |= owner && (a > bk || i > k) && i < m && A.u * fabs(R[a][bk]) > aak;
                     }
-                    need = __ballot(bad) != 0;
+                    need = (__ballot(bad) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange
                         const double dinv = 1.0 / akk;
+                        double lv[RM], cv[RM];
 #pragma unroll
-                        for (int b = bk; b < RM; ++b) cv[b] *= dinv;
+                        for (int a = bk; a < RM; ++a) {
+                            // rows / columns >= m read slack beyond colv: only scratch registers use them
+                            lv[a] = colv[ty + G * a];
+                            cv[a] = colv[tx + G * a] * dinv;
+                        }
+                        if (tx <= kk) cv[bk] = 0.0;  // columns <= k keep their values
 #pragma unroll
                         for (int a = bk; a < RM; ++a)
 #pragma unroll
