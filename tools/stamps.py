@@ -33,6 +33,15 @@ if os.environ.get("MODE") == "2":
         print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} | write: coef {w[s,0].mean():6.2f} L {w[s,1].mean():6.2f} "
               f"rows {w[s,2].mean():6.2f} cb {w[s,3].mean():6.2f} tail {((st[s,3]-st[s,7])*10e-3).mean():6.2f} us")
     sys.exit(0)
+if os.environ.get("MODE") == "4":
+    for lev in range(fl.max() + 1):
+        s = fl == lev
+        a0 = (st[s, 4] - st[s, 0]) * 10e-3
+        a1 = (st[s, 5] - st[s, 4]) * 10e-3
+        a2 = (st[s, 6] - st[s, 5]) * 10e-3
+        print(f"level {lev:2d} m {fm[s].mean():5.1f} | assembly: rows+zero {a0.mean():6.2f} entries {a1.mean():6.2f} "
+              f"children {a2.mean():6.2f} us (total {asm[s].mean():6.2f})")
+    sys.exit(0)
 if os.environ.get("MODE") == "3":
     w4, w5 = st[:, 4], st[:, 5]
     parts = np.stack([w4 & 0xffffffff, w4 >> 32, w5 & 0xffffffff, w5 >> 32, st[:, 6]], 1).astype(np.float64)

@@ -561,11 +561,19 @@ int upload_structure(uno_kkt_t h) {
     const int64_t n = S.n;
     // global scratch for fronts too large for LDS
     std::vector<int64_t> goff(S.nf + 1, 0);
-    int64_t gtot = 8;  // leading pad: element -1 of the first front is the kernels' trash slot
+    int64_t gtot = 0;
     for (int64_t f = 0; f < S.nf; ++f) {
-        goff[f] = gtot;
-        if (S.f_m[f] > kMaxLdsFront) gtot += (int64_t)S.f_m[f] * S.f_m[f];
+        // element -1 of every global front is its own trash slot (masked-off lanes of the assembly
+        // read-add-write it; a slot shared with the previous front would race with that front)
+        if (S.f_m[f] > kMaxLdsFront) {
+            gtot += 8;
+            goff[f] = gtot;
+            gtot += (int64_t)S.f_m[f] * S.f_m[f];
+        } else {
+            goff[f] = gtot;
+        }
     }
+    gtot += 8;
     hipStream_t s = h->stream;
     HIPCHK(h, S.identity_dups ? (h->dup_ptr.release(), hipSuccess) : h->dup_ptr.upload(S.dup_ptr, s));
     HIPCHK(h, h->dup_pos.upload(S.dup_pos, s));

@@ -741,7 +741,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
-        if (!sub) {
+        if (!sub && A.stamp_mode != 4) {
             A.stamps[8 * f + 4] = cyc_search;
             A.stamps[8 * f + 5] = cyc_update;
             A.stamps[8 * f + 6] = cyc_rest;
@@ -916,6 +916,8 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
     }
     for (int64_t t = tid; t < fsize; t += NT) st.F[t] = 0.0;
     __syncthreads();
+    const bool asm_st = A.stamps && A.stamp_mode == 4 && tid == 0;  // diagnostics: assembly sub-phases
+    if (asm_st) A.stamps[8 * f + 4] = __builtin_amdgcn_s_memrealtime();
     // original entries (distinct positions, summed duplicates already packed by k_pack)
     for (int64_t eb = e0 + tid;; eb += (int64_t)EB * NT) {
 #pragma unroll
@@ -934,9 +936,38 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
             uv[q] = e < e1 ? A.uval[e] : 0.0;
         }
     }
+    if (asm_st) { __builtin_amdgcn_s_waitcnt(0); A.stamps[8 * f + 5] = __builtin_amdgcn_s_memrealtime(); }
     // children: contribution blocks are row-major packed lower triangles (row r: columns 0..r);
-    // relmap maps child CB rows to ascending parent rows, so (rm[r], rm[c]) is in the lower triangle
-    constexpr int CB = 8;
+    // relmap maps child CB rows to ascending parent rows, so (rm[r], rm[c]) is in the lower triangle.
+    // Children are taken in pairs whose first batches are loaded together (the loads of a child are
+    // one global round trip, mostly TLB / HBM latency at the upper levels); the additions are applied
+    // child by child in a fixed order (deterministic sums).
+    constexpr int CB = NT == 64 ? 16 : 8;  // entries per lane per batch (one batch covers a 45-row CB at one wave)
+    struct Batch {
+        double v[CB];
+        int pos[CB];
+    };
+    auto load_batch = [&](const double* cb, const int32_t* rm, int ctot, int t0, Batch& b) {
+        int32_t gi[CB], gj[CB];
+#pragma unroll
+        for (int u = 0; u < CB; ++u) {
+            const int t = t0 + u * NT;
+            int r = 0, c = 0;
+            if (t < ctot) tri_rc(t, r, c);
+            b.v[u] = t < ctot ? cb[t] : 0.0;
+            gi[u] = rm[r];
+            gj[u] = rm[c];
+        }
+#pragma unroll
+        for (int u = 0; u < CB; ++u) b.pos[u] = t0 + u * NT < ctot ? st.idx(gi[u], gj[u]) : -1;
+    };
+    auto add_batch = [&](const Batch& b) {
+        double old[CB];
+#pragma unroll
+        for (int u = 0; u < CB; ++u) old[u] = st.F[b.pos[u]];
+#pragma unroll
+        for (int u = 0; u < CB; ++u) st.F[b.pos[u]] = old[u] + b.v[u];
+    };
     for (int cb0 = c0; cb0 < c1; cb0 += 64) {
         if (cb0 != c0 && lane < c1 - cb0) {
             my_cm = A.ch_cm[cb0 + lane];
@@ -944,38 +975,36 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
             my_cbo = (unsigned long long)A.ch_cb_off[cb0 + lane];
         }
         const int nc = c1 - cb0 < 64 ? c1 - cb0 : 64;
-        for (int q = 0; q < nc; ++q) {
-            const int cm = __builtin_amdgcn_readlane(my_cm, q);
-            if (cm <= 0) continue;
-            const int32_t* rm = A.relmap + (int64_t)readlane64(my_rmo, q);
-            const double* cb = A.cb + (int64_t)readlane64(my_cbo, q);
-            const int ctot = cm * (cm + 1) / 2;
-            for (int t0 = tid; t0 < ctot; t0 += NT * CB) {
-                double v[CB];
-                int32_t gi[CB], gj[CB];
-#pragma unroll
-                for (int u = 0; u < CB; ++u) {
-                    const int t = t0 + u * NT;
-                    int r = 0, c = 0;
-                    if (t < ctot) tri_rc(t, r, c);
-                    v[u] = t < ctot ? cb[t] : 0.0;
-                    gi[u] = rm[r];
-                    gj[u] = rm[c];
-                }
-                int pos[CB];
-                double old[CB];
-#pragma unroll
-                for (int u = 0; u < CB; ++u) {
-                    pos[u] = t0 + u * NT < ctot ? st.idx(gi[u], gj[u]) : -1;
-                    old[u] = st.F[pos[u]];
-                }
-#pragma unroll
-                for (int u = 0; u < CB; ++u) st.F[pos[u]] = old[u] + v[u];
+        for (int q = 0; q < nc; q += 2) {
+            const bool two = q + 1 < nc;  // uniform
+            const int cma = __builtin_amdgcn_readlane(my_cm, q);
+            const int cmb = two ? __builtin_amdgcn_readlane(my_cm, q + 1) : 0;
+            const int32_t* rma = A.relmap + (int64_t)readlane64(my_rmo, q);
+            const double* cba = A.cb + (int64_t)readlane64(my_cbo, q);
+            const int32_t* rmb = A.relmap + (two ? (int64_t)readlane64(my_rmo, q + 1) : 0);
+            const double* cbb = A.cb + (two ? (int64_t)readlane64(my_cbo, q + 1) : 0);
+            const int ta = cma > 0 ? cma * (cma + 1) / 2 : 0, tb = cmb > 0 ? cmb * (cmb + 1) / 2 : 0;
+            Batch ba, bb;
+            load_batch(cba, rma, ta, tid, ba);
+            load_batch(cbb, rmb, tb, tid, bb);
+            add_batch(ba);
+            // rest of a / b (CBs of more than 45 rows at one wave): uniform loops, so the barrier
+            // below is reached by every wave
+            for (int base = NT * CB; base < ta; base += NT * CB) {
+                load_batch(cba, rma, ta, base + tid, ba);
+                add_batch(ba);
             }
             if (NT > 64) __syncthreads();  // children may overlap: one child at a time
+            add_batch(bb);
+            for (int base = NT * CB; base < tb; base += NT * CB) {
+                load_batch(cbb, rmb, tb, base + tid, bb);
+                add_batch(bb);
+            }
+            if (NT > 64) __syncthreads();
         }
     }
     __syncthreads();
+    if (asm_st) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // LDS layout of one front: [FrontShared 32 B][packed lower m(m+1)/2, even][sloc m][coefB m]
