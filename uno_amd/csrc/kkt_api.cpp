@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -47,8 +48,9 @@ struct DBuf {
     ~DBuf() { release(); }
 };
 
-enum KernelClass { KC_PACK = 0, KC_SCALE, KC_FACTOR_LDS, KC_FACTOR_GLOBAL, KC_SOLVE_FWD, KC_SOLVE_BWD, KC_RHS, KC_SYMV, KC_COUNT };
-const char* kClassNames[KC_COUNT] = {"pack", "scale", "factor_lds", "factor_global", "solve_fwd", "solve_bwd", "rhs", "symv"};
+enum KernelClass { KC_PACK = 0, KC_SCALE, KC_FACTOR_LDS, KC_FACTOR_GLOBAL, KC_SOLVE_FWD, KC_SOLVE_BWD, KC_RHS, KC_SYMV, KC_ROWSUM, KC_COUNT };
+const char* kClassNames[KC_COUNT] = {"pack", "scale", "factor_lds", "factor_global", "solve_fwd", "solve_bwd", "rhs", "symv",
+                                     "rowsum"};
 
 struct Launch {
     int begin, count, mmax;
@@ -96,6 +98,14 @@ struct DistState {
 struct uno_kkt {
     int device = 0;
     hipStream_t stream = nullptr;
+    // ||A_pre||_inf (row sums of the scaled matrix) runs on stream2 beside the factorization, which uses
+    // threshold 0 and records its smallest accepted pivot; finish_factorization checks it against the
+    // exact threshold and refactors with the exact one in the (rare) case it would have mattered
+    hipStream_t stream2 = nullptr;
+    hipEvent_t ev_scale = nullptr, ev_norm = nullptr;
+    int overlap_norm = 1;
+    bool exact_next = false, last_optimistic = false;
+    int64_t exact_redos = 0;
     AnalysisOptions aopt;
     double u = 0.01, null_fac = 1e-5;
     int scale_iters = 1;
@@ -115,7 +125,8 @@ struct uno_kkt {
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
     DBuf<int32_t> ch_cm;
     DBuf<int8_t> piv;
-    DBuf<unsigned long long> anorm, counters, stamps, fcnt;
+    DBuf<unsigned long long> anorm, counters, stamps, fcnt, minbits;
+    DBuf<double> fmin;
     int want_stamps = 0;
     DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed;
     int32_t n_long = 0;
@@ -173,17 +184,18 @@ hipEvent_t get_event(uno_kkt_t h) {
 struct TimerScope {
     uno_kkt_t h;
     int cls;
+    hipStream_t s;
     hipEvent_t a = nullptr;
-    TimerScope(uno_kkt_t h_, int c) : h(h_), cls(c) {
+    TimerScope(uno_kkt_t h_, int c, hipStream_t st = nullptr) : h(h_), cls(c), s(st ? st : h_->stream) {
         if (h->timing) {
             a = get_event(h);
-            hipEventRecord(a, h->stream);
+            hipEventRecord(a, s);
         }
     }
     ~TimerScope() {
         if (a) {
             hipEvent_t b = get_event(h);
-            hipEventRecord(b, h->stream);
+            hipEventRecord(b, s);
             h->pending.push_back({cls, a, b});
         }
     }
@@ -192,6 +204,7 @@ struct TimerScope {
 void flush_timing(uno_kkt_t h) {
     if (h->pending.empty()) return;
     hipStreamSynchronize(h->stream);
+    if (h->stream2) hipStreamSynchronize(h->stream2);
     for (auto& t : h->pending) {
         float ms = 0.f;
         hipEventElapsedTime(&ms, t.a, t.b);
@@ -470,10 +483,36 @@ int allreduce_host(uno_kkt_t h, std::vector<unsigned long long>& v, RedOp op) {
 }
 
 
+// wait for the factorization; if it ran with the overlapped norm (threshold 0), check that no
+// accepted pivot is at or below the exact null-pivot threshold, else refactor with the exact one
+int sync_and_verify(uno_kkt_t h) {
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    if (h->last_optimistic) {
+        HIPCHK(h, hipEventSynchronize(h->ev_norm));
+        double anorm, mp;
+        memcpy(&anorm, h->h_counters + 9, 8);
+        memcpy(&mp, h->h_counters + 8, 8);
+        const double thres = DBL_EPSILON * h->null_fac * anorm;
+        if (!(mp > thres)) {
+            h->exact_next = true;
+            int rc = enqueue_factorization(h);
+            h->exact_next = false;
+            if (rc != UNO_KKT_OK) return rc;
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            h->exact_redos++;
+            if (h->verbose) fprintf(stderr, "[uno_kkt] pivot %.3e <= null threshold %.3e: refactored exactly\n", mp, thres);
+        }
+    }
+    flush_timing(h);
+    return UNO_KKT_OK;
+}
+
 int finish_factorization(uno_kkt_t h) {
     if (!h->factor_enqueued) return h->factored ? UNO_KKT_OK : set_err(h, UNO_KKT_ERR_STATE, "no factorization");
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    flush_timing(h);
+    {
+        int rc = sync_and_verify(h);
+        if (rc != UNO_KKT_OK) return rc;
+    }
     h->factor_enqueued = false;
     // delayed pivots: a front that could not pivot a fully-summed column (or, optionally, needed a
     // relaxed threshold) is amalgamated into its parent and the factorization is redone.  The merge
@@ -526,8 +565,7 @@ int finish_factorization(uno_kkt_t h) {
         auto tu = std::chrono::steady_clock::now();
         rc = enqueue_factorization(h);
         if (rc != UNO_KKT_OK) return rc;
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        flush_timing(h);
+        if ((rc = sync_and_verify(h)) != UNO_KKT_OK) return rc;
         h->factor_enqueued = false;
         if (h->verbose)
             fprintf(stderr, "[uno_kkt] merge round %d: %lld delayed columns listed, %lld moved, stuck %llu; "
@@ -607,6 +645,9 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->gscratch_off.upload(goff, s));
     HIPCHK(h, h->fstat.alloc(S.nf));
     HIPCHK(h, h->fcnt.alloc(S.nf));
+    HIPCHK(h, h->fmin.alloc(S.nf));
+    if (S.nf > 0) HIPCHK(h, hipMemsetAsync(h->fmin.p, 0x7f, sizeof(double) * S.nf, s));  // 1.4e306: above any threshold
+    if (!h->minbits.p) HIPCHK(h, h->minbits.alloc(1));
     HIPCHK(h, h->perm_d.upload(S.perm, s));
     HIPCHK(h, h->cptr.upload(S.cptr, s));
     HIPCHK(h, h->rptr.upload(S.rptr, s));
@@ -699,9 +740,22 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.rslot = h->rslot.p; SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p;
         SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p;
         SA.n_long = h->n_long; SA.max_long = h->max_long;
-        if (h->world == 1) {
+        if (h->world == 1 && h->overlap_norm && !h->exact_next) {
+            HIPCHK(h, launch_scale_sweeps(SA, h->scale_iters, h->rmax.p, s));
+            HIPCHK(h, hipEventRecord(h->ev_scale, s));
+            HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_scale, 0));
+            {
+                TimerScope t2(h, KC_ROWSUM, h->stream2);
+                HIPCHK(h, launch_rowsum_norm(SA, h->rowsum.p, h->stream2));
+            }
+            HIPCHK(h, hipMemcpyAsync(h->h_counters + 9, h->anorm.p, 8, hipMemcpyDeviceToHost, h->stream2));
+            HIPCHK(h, hipEventRecord(h->ev_norm, h->stream2));
+            h->last_optimistic = true;
+        } else if (h->world == 1) {
             HIPCHK(h, launch_scale(SA, h->scale_iters, h->rmax.p, h->rowsum.p, s));
+            h->last_optimistic = false;
         } else {
+            h->last_optimistic = false;
             int rc = dist_scale(h, SA);
             if (rc != UNO_KKT_OK) return rc;
         }
@@ -714,6 +768,8 @@ int enqueue_factorization(uno_kkt_t h) {
     A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
+    A.fmin = h->fmin.p;
+    if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     A.stamps = nullptr;
     A.stamp_mode = h->want_stamps;
@@ -736,13 +792,15 @@ int enqueue_factorization(uno_kkt_t h) {
             HIPCHK(h, launch_factor(A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
         }
     }
-    HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, S.nf, h->counters.p, s));
+    HIPCHK(h, hipMemsetAsync(h->minbits.p, 0xff, 8, s));
+    HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits.p, s));
     if (h->world > 1) {
         // counters[7] keeps this rank's delayed-column count; 0..6 are summed over the ranks
         HIPCHK(h, hipMemcpyAsync(h->counters.p + 7, h->counters.p + 6, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
         HIPCHK(h, h->comm->allreduce(h->counters.p, 7, RedOp::SumU64, s));
     }
     HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipMemcpyAsync(h->h_counters + 8, h->minbits.p, 8, hipMemcpyDeviceToHost, s));
     h->factor_enqueued = true;
     return UNO_KKT_OK;
 }
@@ -763,11 +821,14 @@ int uno_kkt_create(uno_kkt_t* handle, int device_id) {
     auto* h = new uno_kkt();
     h->device = device_id;
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_counters, 8 * sizeof(unsigned long long)) != hipSuccess) {
+        hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_scale, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_norm, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_counters, 10 * sizeof(unsigned long long)) != hipSuccess) {
         delete h;
         return UNO_KKT_ERR_HIP;
     }
-    memset(h->h_counters, 0, 8 * sizeof(unsigned long long));
+    memset(h->h_counters, 0, 10 * sizeof(unsigned long long));
     *handle = h;
     return UNO_KKT_OK;
 }
@@ -779,6 +840,10 @@ void uno_kkt_destroy(uno_kkt_t h) {
     for (auto& t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
     if (h->h_counters) hipHostFree(h->h_counters);
+    if (h->stream2) hipStreamSynchronize(h->stream2);
+    if (h->ev_scale) hipEventDestroy(h->ev_scale);
+    if (h->ev_norm) hipEventDestroy(h->ev_norm);
+    if (h->stream2) hipStreamDestroy(h->stream2);
     delete h->comm;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -799,6 +864,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else if (n == "gather_solution") h->gather_solution = value != 0.0;
     else if (n == "verbose") h->verbose = (int)value;
+    else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;
 }
@@ -907,6 +973,10 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     HIPCHK(h, hipSetDevice(h->device));
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
+    if (h->factor_enqueued) {  // the factorization is final only once checked (delays, null threshold)
+        int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK) return rc;
+    }
     const double* b = rhs;
     if (!on_device) {
         if (S.n > 0) HIPCHK(h, hipMemcpyAsync(h->bvec.p, rhs, S.n * sizeof(double), hipMemcpyHostToDevice, s));
@@ -981,10 +1051,6 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     if (!on_device) {
         if (S.n > 0) HIPCHK(h, hipMemcpyAsync(x, xd, S.n * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
-    }
-    if (h->factor_enqueued) {
-        int rc = finish_factorization(h);
-        if (rc != UNO_KKT_OK) return rc;
     }
     return UNO_KKT_OK;
 }

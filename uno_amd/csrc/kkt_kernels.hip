@@ -274,7 +274,7 @@ __device__ __forceinline__ unsigned long long argmax_key(double av, int i) {
 // wave-uniform.  Mirrors test_pivot() of oracle/kkt_oracle.c; the relaxed ladder is only used at
 // roots or when delays are disabled (otherwise the first relaxation reports the delayed columns).
 template <class S>
-__device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u, double thres) {
+__device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u, double thres, double& minpiv) {
     const int lane = threadIdx.x & 63;
     PivotDecision d{PIV_STUCK, k, -1, 0};
     for (int ul = 0; ul < 6; ++ul) {
@@ -289,6 +289,7 @@ __device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u
             g = wave_max_abs(g);
             const double acc = fabs(st.at(c, c));
             if (fmax(acc, g) <= thres) { d.kind = PIV_NULL; d.c = c; d.relaxed = ul > 0; return d; }
+            minpiv = fmin(minpiv, fmax(acc, g));  // a larger null threshold would have stopped here
             if (acc != 0.0 && acc >= uu * g) { d.kind = PIV_1X1; d.c = c; d.relaxed = ul > 0; return d; }
             // 1x1 rejected: largest off-diagonal among the fully-summed rows is the 2x2 partner
             unsigned long long key = 0;
@@ -493,7 +494,11 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     const int tid = threadIdx.x;
     for (int i = tid; i < m; i += NT) lorig[i] = i;  // local position before pivoting
     __syncthreads();
-    const double thres = DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits);
+    // null-pivot threshold eps * null_fac * ||A_pre||_inf; with anorm_bits == nullptr the norm is still
+    // being computed on a second stream: the front is factored with threshold 0 and records the
+    // smallest pivot magnitude it accepted (minpiv), which the host checks against the exact threshold
+    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+    double minpiv = INFINITY;
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
     bool delays_recorded = false;
     // diagnostics (stamps build path only): shader-clock cycles spent in search / update / rest
@@ -547,6 +552,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     need = (__ballot(bad) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange
+                        minpiv = fmin(minpiv, aak);
                         const double dinv = 1.0 / akk;
                         double lv[RM], cv[RM];
 #pragma unroll
@@ -621,6 +627,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     }
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange: rank-1 update in registers
+                        minpiv = fmin(minpiv, aak);
                         const double dinv = 1.0 / akk;
 #pragma unroll
                         for (int b = bk; b < RM; ++b) cv[b] *= dinv;
@@ -643,8 +650,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             PivotDecision d;
             if (!REG && quick_1x1(st, m, k, A.u, thres)) {
                 d = PivotDecision{PIV_1X1, k, -1, 0};
+                minpiv = fmin(minpiv, fabs(st.at(k, k)));
             } else {
-                d = search_pivot(st, m, k, p, A.u, thres);
+                d = search_pivot(st, m, k, p, A.u, thres, minpiv);
             }
             if (tid == 0) sh->dec = d;
         }
@@ -879,6 +887,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         // serialize on the counters' cache line and stall every access routed to that L2 channel
         A.fcnt[f] = (unsigned long long)npos | (unsigned long long)nneg << 16 | (unsigned long long)nzero << 32 |
                     (unsigned long long)n2 << 48;
+        A.fmin[f] = minpiv;
     }
 }
 
@@ -1456,7 +1465,7 @@ hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int
     return hipGetLastError();
 }
 
-hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s) {
+hipError_t launch_scale_sweeps(ScanArgs A, int iters, double* rmax, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     for (int it = 0; it < iters; ++it) {
         A.out = rmax;
@@ -1468,10 +1477,20 @@ hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hip
         hipMemsetAsync(rmax, 0, sizeof(double) * A.n, s);
         launch_scale_update(rmax, A.scale, nullptr, A.n, 1, s);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_rowsum_norm(ScanArgs A, double* rowsum, hipStream_t s) {
+    if (A.n == 0) return hipSuccess;
     A.out = rowsum;
     hipError_t e = launch_rowscan(A, 2, s);
     if (e != hipSuccess) return e;
     return launch_normmax(rowsum, nullptr, A.n, A.anorm, s);
+}
+
+hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s) {
+    hipError_t e = launch_scale_sweeps(A, iters, rmax, s);
+    return e != hipSuccess ? e : launch_rowsum_norm(A, rowsum, s);
 }
 
 size_t factor_lds_bytes(int mmax) {
@@ -1499,10 +1518,14 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
 }
 
 __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restrict__ fcnt,
-                                               const int32_t* __restrict__ fstat, int64_t nf,
-                                               unsigned long long* __restrict__ counters) {
+                                               const int32_t* __restrict__ fstat, const double* __restrict__ fmin,
+                                               int64_t nf, unsigned long long* __restrict__ counters,
+                                               unsigned long long* __restrict__ minbits) {
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
+    unsigned long long mn = ~0ull;
     for (int64_t f = blockIdx.x * 256 + threadIdx.x; f < nf; f += (int64_t)gridDim.x * 256) {
+        const unsigned long long fm = as_bits(fmin[f]);  // non-negative doubles order like their bits
+        mn = fm < mn ? fm : mn;
         const unsigned long long c = fcnt[f];
         const uint32_t st = (uint32_t)fstat[f];
         acc[0] += c & 0xffff; acc[1] += (c >> 16) & 0xffff; acc[2] += (c >> 32) & 0xffff; acc[3] += c >> 48;
@@ -1515,18 +1538,29 @@ __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restr
         for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
         if ((threadIdx.x & 63) == 0) red[q][threadIdx.x >> 6] = v;
     }
+    __shared__ unsigned long long rmin[4];
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long x = __shfl_xor(mn, o);
+        mn = x < mn ? x : mn;
+    }
+    if ((threadIdx.x & 63) == 0) rmin[threadIdx.x >> 6] = mn;
     __syncthreads();
     if (threadIdx.x < 6) {
         const unsigned long long v = red[threadIdx.x][0] + red[threadIdx.x][1] + red[threadIdx.x][2] + red[threadIdx.x][3];
         if (v) atomicAdd(counters + threadIdx.x, v);
     }
+    if (threadIdx.x == 6 && minbits) {
+        unsigned long long v = rmin[0];
+        for (int w = 1; w < 4; ++w) v = rmin[w] < v ? rmin[w] : v;
+        atomicMin(minbits, v);
+    }
 }
 
-hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, int64_t nf, unsigned long long* counters,
-                        hipStream_t s) {
+hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
+                        unsigned long long* counters, unsigned long long* minbits, hipStream_t s) {
     if (nf <= 0) return hipSuccess;
     const int blocks = (int)std::min<int64_t>(64, (nf + 255) / 256);
-    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, nf, counters);
+    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, fmin, nf, counters, minbits);
     return hipGetLastError();
 }
 

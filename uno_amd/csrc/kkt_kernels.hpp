@@ -27,7 +27,7 @@ struct FactorArgs {
     const int64_t* L_off;
     const int64_t* cb_off;
     const int64_t* gscratch_off;  // per front, only used by k_factor_global
-    const unsigned long long* anorm_bits;
+    const unsigned long long* anorm_bits;  // ||A_pre||_inf; nullptr = threshold 0 + minpiv record (norm overlapped)
     double* L;
     double* cb;
     double* gscratch;
@@ -37,6 +37,7 @@ struct FactorArgs {
     unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck, delayed
     int32_t* fstat;             // per front: stuck pivots (low 16 bits) | relaxed pivots (high 16 bits)
     unsigned long long* fcnt;   // per front: npos | nneg << 16 | nzero << 32 | n2x2 << 48 (summed by launch_count)
+    double* fmin;               // per front: smallest pivot magnitude accepted as non-null (min by launch_count)
     const int32_t* fparent;     // assembly-tree parent (-1 = root)
     int32_t* delayed;           // original ids of columns that failed the threshold (counters[6] = count)
     int record_delays;
@@ -105,6 +106,9 @@ hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32
                        double* uval, hipStream_t s);
 // single-GPU equilibration: `iters` max-scaling sweeps over all rows, then row sums and ||A_pre||_inf
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s);
+// the two halves of launch_scale: scaling sweeps (scale ready), then row sums + ||A_pre||_inf
+hipError_t launch_scale_sweeps(ScanArgs A, int iters, double* rmax, hipStream_t s);
+hipError_t launch_rowsum_norm(ScanArgs A, double* rowsum, hipStream_t s);
 // building blocks of the distributed equilibration (mode 0: max |a|, 1: max |s a s|, 2: sum |s a s|)
 hipError_t launch_rowscan(const ScanArgs& A, int mode, hipStream_t s);
 hipError_t launch_rowscan_part(const PartArgs& A, int mode, hipStream_t s);
@@ -119,8 +123,8 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
 hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int count, int lds_doubles, bool forward,
                              hipStream_t s);
 // counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
-hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, int64_t nf, unsigned long long* counters,
-                        hipStream_t s);
+hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
+                        unsigned long long* counters, unsigned long long* minbits, hipStream_t s);
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
