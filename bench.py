@@ -47,6 +47,7 @@ def parse():
     ap.add_argument("--profile-only", action="store_true", help="skip event pass and CPU baseline")
     ap.add_argument("--leaf", type=int, default=0, help="nested-dissection leaf size (0 = library default)")
     ap.add_argument("--block", type=int, default=0, help="max supernode width (0 = library default)")
+    ap.add_argument("--dataflow", type=int, default=1, help="1: one-launch dataflow solve, 0: level-scheduled solve")
     return ap.parse_args()
 
 
@@ -82,6 +83,7 @@ def main():
         kkt.set_option("leaf_size", args.leaf)
     if args.block:
         kkt.set_option("max_block", args.block)
+    kkt.set_option("dataflow_solve", args.dataflow)
     t0 = time.perf_counter()
     kkt.analyze(n, rows, cols)
     t_analysis = time.perf_counter() - t0
@@ -209,6 +211,7 @@ def main():
                    "max_front": st["max_front"], "ordering": "nested dissection (BFS level sets), 6 dense nodes last",
                    "analysis_s": round(t_analysis, 3), "inertia": list(inertia),
                    "pivots_2x2": st["pivots_2x2"], "pivots_relaxed": st["pivots_relaxed"],
+                   "solve_schedule": f"dataflow grid {st['solve_grid']}" if st["solve_grid"] else "level-synchronous",
                    "fronts_merged": st["fronts_merged"], "rel_residual": rel_res,
                    "parallelism": (f"subtree-partitioned x{world} (RCCL root exchange to rank 0)" if dist_mode
                                    else f"replicas x{world} (independent KKT per GPU)"),

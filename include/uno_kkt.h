@@ -52,6 +52,8 @@ typedef struct {
     double bytes_L;         /* 8 * stored factor entries (L + D) */
     double bytes_cb;        /* 8 * contribution-block entries written per factorization */
     int64_t fronts_merged;  /* fronts amalgamated into their parent since analysis (delayed pivots) */
+    int64_t solve_grid;     /* dataflow solve: resident one-wave blocks per direction (0 = level-scheduled) */
+    int64_t solve_aborts;   /* dataflow solves abandoned at the dependency-wait limit (then level-scheduled) */
 } uno_kkt_stats_t;
 
 /* Create a solver bound to HIP device `device_id`.  Replaces MUMPS JOB=-1 (MUMPSSolver.cpp:16-37). */

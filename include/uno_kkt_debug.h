@@ -19,6 +19,9 @@ int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const i
                              int32_t* front_pivots, int32_t* front_level, int64_t cap);
 int64_t uno_kkt_debug_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap, int32_t* front_order,
                              int32_t* front_pivots, int32_t* front_level);
+/* Option "solve_stamps" = 1: per front 8 words of the last dataflow solve, s_memrealtime (100 MHz) at
+ * {start, dependency satisfied, values staged, published} of the forward (0..3) and backward (4..7) pass. */
+int64_t uno_kkt_debug_solve_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap);
 #ifdef __cplusplus
 }
 #endif

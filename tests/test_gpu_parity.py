@@ -180,3 +180,31 @@ def test_empty_and_tiny(uno_amd):
     g.factorize([-2.0])
     assert g.inertia() == (0, 1, 0)
     np.testing.assert_allclose(g.solve([4.0]), [-2.0])
+
+
+@pytest.mark.parametrize("n", [10000, 200000])
+def test_dataflow_solve_matches_level_schedule(uno_amd, n):
+    """The one-launch dataflow solve (k_solve_*_df: fronts wait on arrival counters inside the launch)
+    does the same arithmetic as the level-scheduled launches: solutions bit-identical, over repeated
+    solves (cumulative epoch counters) and after a refactorization with other values (new pivoting)."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    N, nv, m, r, c, v, b = arrowband(n, SEEDS["C2"])
+    gd, gl = HipKKT(0), HipKKT(0, dataflow_solve=0)
+    for g in (gd, gl):
+        g.analyze(N, r, c)
+        g.factorize(v)
+    assert gd.stats()["solve_grid"] > 0 and gl.stats()["solve_grid"] == 0
+    xl = gl.solve(b)
+    for rep in range(3):
+        xd = gd.solve(b * (rep + 1))
+        np.testing.assert_array_equal(xd, gl.solve(b * (rep + 1)) if rep else xl)
+    assert rel_residual(N, r, c, v, xl, b) < RES_TOL
+    v2 = v.copy()
+    v2[:nv] = 1e-2
+    v2[nv:N] = -1e-9
+    for g in (gd, gl):
+        g.factorize(v2)
+    assert gd.inertia() == gl.inertia()
+    b2 = np.cos(np.arange(N))
+    np.testing.assert_array_equal(gd.solve(b2), gl.solve(b2))
+    assert gd.stats()["solve_aborts"] == 0

@@ -133,6 +133,20 @@ struct uno_kkt {
     int64_t max_long = 0;
     unsigned long long* h_counters = nullptr;
     Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
+    // dataflow solve (one launch per direction, kkt_kernels.hip k_solve_*_df); single GPU, every front
+    // one-wave eligible; option "dataflow_solve" (default 1)
+    int df_enabled = 1;
+    int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
+    uint32_t df_epoch = 0;
+    bool df_rx_valid = false;      // rxpos matches the last factorization's pivoting
+    bool df_check = false;         // a dataflow solve's abort flag copy is pending
+    int64_t df_aborts = 0;
+    DBuf<int32_t> df_order, df_xpos, df_rxpos;
+    DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
+    DBuf<uint32_t> df_cnt, df_done, df_abort;
+    DBuf<double> df_cvx, df_xs;
+    int want_solve_stamps = 0;
+    DBuf<unsigned long long> df_stamps;
     // distributed factorization (null comm: one GPU)
     // device-side vector work around the solve
     int64_t rhs_n = -1, rhs_m = -1;
@@ -218,6 +232,33 @@ void flush_timing(uno_kkt_t h) {
 
 int upload_structure(uno_kkt_t h);
 int enqueue_factorization(uno_kkt_t h);
+
+DfArgs dataflow_args(uno_kkt_t h) {
+    DfArgs D;
+    D.order = h->df_order.p; D.nf = (int32_t)h->S.nf; D.parent = h->fparent.p; D.cnt = h->df_cnt.p;
+    D.done = h->df_done.p; D.epoch = h->df_epoch; D.cvx = h->df_cvx.p; D.cvx_off = h->df_cvx_off.p;
+    D.ch_cvx_off = h->df_ch_cvx_off.p; D.xs = h->df_xs.p; D.xs_off = h->df_xs_off.p; D.rxpos = h->df_rxpos.p;
+    D.abort_flag = h->df_abort.p;
+    D.stamps = h->want_solve_stamps ? h->df_stamps.p : nullptr;
+    return D;
+}
+
+// After the stream has drained: a dataflow solve whose waits hit their limit produced no valid
+// solution; the counters are cleared and the level schedule is used from then on.
+int check_dataflow(uno_kkt_t h) {
+    h->df_check = false;
+    uint32_t ab = 0;
+    memcpy(&ab, h->h_counters + 10, sizeof(ab));
+    if (ab == 0) return UNO_KKT_OK;
+    h->df_aborts++;
+    h->df_enabled = 0;
+    h->df_grid = 0;
+    memset(h->h_counters + 10, 0, 8);
+    HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    return set_err(h, UNO_KKT_ERR_HIP, "dataflow solve aborted (dependency wait limit): the last device solution is "
+                                       "invalid; level-scheduled solves from now on");
+}
 
 // Launch plan of the fronts selected by `take`: per level, fronts sorted by order (descending) cut
 // into size classes -- factor: one kernel instance per LDS class; solve: one-wave kernels grouped by
@@ -591,6 +632,56 @@ int finish_factorization(uno_kkt_t h) {
     return UNO_KKT_OK;
 }
 
+// Dataflow solve layout: topological front order (the level order), 128-byte-aligned per-front slots
+// for the forward update vectors and the backward solution values, arrival counters.
+hipError_t setup_dataflow(uno_kkt_t h) {
+    const Symbolic& S = h->S;
+    h->df_grid = 0;
+    h->df_rx_valid = false;
+    h->df_epoch = 0;
+    if (h->world > 1 || !h->df_enabled || S.nf == 0) return hipSuccess;
+    int lds = 0;
+    for (int64_t f = 0; f < S.nf; ++f) {
+        const int m = S.f_m[f], p = S.f_p[f];
+        if (p > 64 || m > kMaxLdsFront) {  // a front needs the 256-thread kernels
+            if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve off: front %lld m %d p %d\n", (long long)f, m, p);
+            return hipSuccess;
+        }
+        const int sz = p * m - p * (p - 1) / 2;
+        lds = std::max(lds, ((sz + 1) & ~1) + ((m + 1) & ~1) + (m + 1) / 2);
+    }
+    std::vector<int64_t> cvx(S.nf), xs(S.nf), chx(S.child.size());
+    int64_t tc = 0, tx = 0;
+    for (int64_t f = 0; f < S.nf; ++f) {
+        cvx[f] = tc;
+        tc += (S.f_m[f] - S.f_p[f] + 15) & ~15;
+        xs[f] = tx;
+        tx += (S.f_p[f] + 15) & ~15;
+    }
+    if (tx >= INT32_MAX) return hipSuccess;
+    for (size_t q = 0; q < S.child.size(); ++q) chx[q] = cvx[S.child[q]];
+    hipStream_t s = h->stream;
+    hipError_t e;
+    if ((e = h->df_order.upload(S.level_fronts, s)) != hipSuccess) return e;
+    if ((e = h->df_cvx_off.upload(cvx, s)) != hipSuccess) return e;
+    if ((e = h->df_ch_cvx_off.upload(chx, s)) != hipSuccess) return e;
+    if ((e = h->df_xs_off.upload(xs, s)) != hipSuccess) return e;
+    if ((e = h->df_cvx.alloc(std::max<int64_t>(tc, 16))) != hipSuccess) return e;
+    if ((e = h->df_xs.alloc(std::max<int64_t>(tx, 16))) != hipSuccess) return e;
+    if ((e = h->df_xpos.alloc(std::max<int64_t>(S.n, 1))) != hipSuccess) return e;
+    if ((e = h->df_rxpos.alloc(std::max<size_t>(S.rows.size(), 1))) != hipSuccess) return e;
+    if ((e = h->df_cnt.alloc(S.nf)) != hipSuccess) return e;
+    if ((e = h->df_done.alloc(S.nf)) != hipSuccess) return e;
+    if (!h->df_abort.p && (e = h->df_abort.alloc(1)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(h->df_cnt.p, 0, sizeof(uint32_t) * S.nf, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(h->df_done.p, 0, sizeof(uint32_t) * S.nf, s)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    h->df_lds = lds;
+    h->df_grid = solve_df_grid(lds, (int)S.nf);
+    if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve: %lld fronts, lds %d doubles, grid %d\n", (long long)S.nf, lds, h->df_grid);
+    return hipSuccess;
+}
+
 int upload_structure(uno_kkt_t h) {
     Symbolic& S = h->S;
     if (S.max_m > kMaxGlobalFront)
@@ -688,6 +779,7 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, hipMemsetAsync(h->fstat.p, 0, sizeof(int32_t) * S.nf, s));
         HIPCHK(h, hipMemsetAsync(h->fcnt.p, 0, sizeof(unsigned long long) * S.nf, s));
     }
+    HIPCHK(h, setup_dataflow(h));
     if (h->world > 1) {
         int rc = setup_distribution(h);
         if (rc != UNO_KKT_OK) return rc;
@@ -802,6 +894,7 @@ int enqueue_factorization(uno_kkt_t h) {
     HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipMemcpyAsync(h->h_counters + 8, h->minbits.p, 8, hipMemcpyDeviceToHost, s));
     h->factor_enqueued = true;
+    h->df_rx_valid = false;  // pivoting may have permuted rows
     return UNO_KKT_OK;
 }
 
@@ -824,11 +917,11 @@ int uno_kkt_create(uno_kkt_t* handle, int device_id) {
         hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_scale, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_norm, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_counters, 10 * sizeof(unsigned long long)) != hipSuccess) {
+        hipHostMalloc((void**)&h->h_counters, 12 * sizeof(unsigned long long)) != hipSuccess) {
         delete h;
         return UNO_KKT_ERR_HIP;
     }
-    memset(h->h_counters, 0, 10 * sizeof(unsigned long long));
+    memset(h->h_counters, 0, 12 * sizeof(unsigned long long));
     *handle = h;
     return UNO_KKT_OK;
 }
@@ -865,6 +958,14 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "gather_solution") h->gather_solution = value != 0.0;
     else if (n == "verbose") h->verbose = (int)value;
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
+    else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
+    else if (n == "dataflow_solve") {
+        h->df_enabled = value != 0.0;
+        if (h->analyzed) {
+            HIPCHK(h, setup_dataflow(h));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+    }
     else return set_err(h, UNO_KKT_ERR_ARG, "unknown option '" + n + "'");
     return UNO_KKT_OK;
 }
@@ -968,6 +1069,11 @@ int uno_kkt_inertia(uno_kkt_t h, int64_t* positive, int64_t* negative, int64_t* 
 
 int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     if (!h || !rhs || !x) return UNO_KKT_ERR_ARG;
+    if (h->df_check) {  // the previous (device-pointer) dataflow solve: aborted waits invalidate it
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        int rc = check_dataflow(h);
+        if (rc != UNO_KKT_OK) return rc;
+    }
     if (!h->analyzed || (!h->factored && !h->factor_enqueued))
         return set_err(h, UNO_KKT_ERR_STATE, "solve before factorize");
     HIPCHK(h, hipSetDevice(h->device));
@@ -982,10 +1088,7 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         if (S.n > 0) HIPCHK(h, hipMemcpyAsync(h->bvec.p, rhs, S.n * sizeof(double), hipMemcpyHostToDevice, s));
         b = h->bvec.p;
     }
-    {
-        TimerScope t(h, KC_RHS);
-        HIPCHK(h, launch_rhs_scale(b, h->scale.p, h->w.p, S.n, s));
-    }
+    const bool df = h->world == 1 && h->df_enabled && h->df_grid > 0;
     SolveArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
@@ -998,7 +1101,37 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     };
     const Plan& P0 = h->plan[0];
     const Plan& P1 = h->plan[1];
-    for (size_t q = 0; q < P0.sol.size(); ++q) {
+    if (!df) {
+        TimerScope t(h, KC_RHS);
+        HIPCHK(h, launch_rhs_scale(b, h->scale.p, h->w.p, S.n, s));
+    }
+    if (df) {
+        DfArgs D = dataflow_args(h);
+        if (!h->df_rx_valid) {
+            HIPCHK(h, launch_xpos(A, D, h->df_xpos.p, h->df_rxpos.p, s));
+            h->df_rx_valid = true;
+        }
+        {
+            TimerScope t(h, KC_RHS);
+            HIPCHK(h, launch_xs_in(b, h->scale.p, h->df_xpos.p, h->df_xs.p, S.n, s));
+        }
+        D.epoch = ++h->df_epoch;
+        if (h->want_solve_stamps) {
+            if (h->df_stamps.n != (size_t)(8 * S.nf)) HIPCHK(h, h->df_stamps.alloc(8 * S.nf));
+            D.stamps = h->df_stamps.p;
+        }
+        {
+            TimerScope t(h, KC_SOLVE_FWD);
+            HIPCHK(h, launch_solve_df(A, D, h->df_grid, h->df_lds, true, s));
+        }
+        {
+            TimerScope t(h, KC_SOLVE_BWD);
+            HIPCHK(h, launch_solve_df(A, D, h->df_grid, h->df_lds, false, s));
+        }
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        h->df_check = true;
+    }
+    for (size_t q = 0; q < P0.sol.size() && !df; ++q) {
         TimerScope t(h, KC_SOLVE_FWD);
         HIPCHK(h, run(P0, P0.sol[q], true));
     }
@@ -1023,14 +1156,15 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
             if (h->rank != 0) HIPCHK(h, launch_scatter(D.tbuf.p, D.top_orig.p, h->w.p, D.n_top_rows, s));
         }
     }
-    for (size_t q = P0.sol.size(); q-- > 0;) {
+    for (size_t q = P0.sol.size(); q-- > 0 && !df;) {
         TimerScope t(h, KC_SOLVE_BWD);
         HIPCHK(h, run(P0, P0.sol[q], false));
     }
     double* xd = on_device ? x : h->bvec.p;
     {
         TimerScope t(h, KC_RHS);
-        HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
+        if (df) HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, xd, S.n, s));
+        else HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
     }
     if (h->world > 1 && h->gather_solution) {
         // MUMPS-style centralized solution on rank 0 (ICNTL(21) = 0): own rows of every other rank
@@ -1051,6 +1185,10 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     if (!on_device) {
         if (S.n > 0) HIPCHK(h, hipMemcpyAsync(x, xd, S.n * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
+        if (df && check_dataflow(h) != UNO_KKT_OK) {
+            h->err.clear();
+            return uno_kkt_solve(h, rhs, x, on_device);  // level schedule (dataflow now disabled)
+        }
     }
     return UNO_KKT_OK;
 }
@@ -1060,6 +1198,8 @@ int uno_kkt_stats(uno_kkt_t h, uno_kkt_stats_t* out) {
     if (h->factor_enqueued) finish_factorization(h);
     *out = h->st;
     out->fronts_merged = h->merges_total;
+    out->solve_grid = (h->world == 1 && h->df_enabled) ? h->df_grid : 0;
+    out->solve_aborts = h->df_aborts;
     return UNO_KKT_OK;
 }
 
@@ -1110,7 +1250,10 @@ int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const i
                              int32_t* flevel, int64_t cap) {
     Pattern P;
     Symbolic S;
-    if (!ukkt::analyze(n, nnz, row, col, AnalysisOptions(), P, S).empty()) return -1;
+    AnalysisOptions opt;  // defaults; UNO_KKT_LEAF / UNO_KKT_BLOCK override them for layout studies
+    if (const char* e = getenv("UNO_KKT_LEAF")) opt.leaf_size = std::max(1, atoi(e));
+    if (const char* e = getenv("UNO_KKT_BLOCK")) opt.max_block = std::max(1, atoi(e));
+    if (!ukkt::analyze(n, nnz, row, col, opt, P, S).empty()) return -1;
     if (cap < S.nf) return -S.nf;
     for (int64_t f = 0; f < S.nf; ++f) { fm[f] = S.f_m[f]; fp[f] = S.f_p[f]; flevel[f] = S.f_level[f]; }
     return S.nf;
@@ -1124,6 +1267,16 @@ int64_t uno_kkt_debug_stamps(uno_kkt_t h, uint64_t* out, int64_t cap, int32_t* f
     if (cap < 8 * nf) return -(8 * nf);
     hipMemcpy(out, h->stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost);
     for (int64_t f = 0; f < nf; ++f) { fm[f] = h->S.f_m[f]; fp[f] = h->S.f_p[f]; flevel[f] = h->S.f_level[f]; }
+    return nf;
+}
+
+// diagnostics: per front {fwd start, dependency met, staged, published, bwd ...} of the last dataflow solve
+int64_t uno_kkt_debug_solve_stamps(uno_kkt_t h, uint64_t* out, int64_t cap) {
+    if (!h || !h->df_stamps.p) return -1;
+    const int64_t nf = h->S.nf;
+    if (cap < 8 * nf) return -(8 * nf);
+    hipStreamSynchronize(h->stream);
+    hipMemcpy(out, h->df_stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost);
     return nf;
 }
 

@@ -11,7 +11,10 @@
 // with butterfly shuffles, the rank-1/rank-2 Schur updates are spread over a 16x16 thread grid.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 
 #include "kkt_kernels.hpp"
@@ -1237,60 +1240,97 @@ __global__ __launch_bounds__(kThreads) void k_solve_bwd(SolveArgs A, const int32
 // coalesced pass -- every load of the panel in flight at once instead of one round trip per column --
 // and the triangle, rectangle and diagonal then run from LDS: lane i owns row i of the triangle,
 // pivots are broadcast with readlane, no barriers beyond the staging one.
+//
+// Two schedules share the per-front bodies below:
+//   level-synchronous (DF = false): one launch per level and LDS class, a block per front;
+//   dataflow (DF = true): ONE launch per direction, a resident grid of one-wave blocks walking the
+//     fronts in a topological order (block b takes positions b, b + grid, ...).  A front waits only
+//     for fronts earlier in that order, so with every block resident (grid sized from the occupancy
+//     query) the earliest unfinished front can always proceed.  Hand-offs inside the launch
+//     (forward: children's update vectors; backward: ancestors' solution values) are written with
+//     sc1 (write-through) stores into 128-byte-aligned per-front slots, read with sc1 loads, and
+//     signalled after the storing wave's vmcnt(0) by one lane: an agent-scope add on the parent's
+//     arrival counter (forward) or an sc1 epoch store (backward), polled with sc1 loads
+//     (MI355X_MICROARCH.md, inter-workgroup visibility, first row of the hand-off table).
+//     Every wait is bounded: past the limit the wave raises abort_flag and every waiter returns, the
+//     host reports the abort and falls back to the level schedule.
 __device__ __forceinline__ int pcol(int m, int k) { return k * m - k * (k - 1) / 2 - k; }  // P[pcol + i] = L(i,k)
 
+// Panel -> LDS: 16-byte loads (after one leading double when the panel starts on an odd double), up
+// to 16 per lane issued before the first LDS write.
 __device__ __forceinline__ void stage_panel(const double* __restrict__ L, int64_t Lo, int sz, double* P) {
     const int lane = threadIdx.x;
-    int t = lane;
-    for (; t + 7 * 64 < sz; t += 8 * 64) {
-        double v[8];
+    const int head = (int)(Lo & 1) < sz ? (int)(Lo & 1) : sz;
+    if (head && lane == 0) P[0] = L[Lo];
+    const int npair = (sz - head) >> 1;
+    if (((sz - head) & 1) && lane == 0) P[sz - 1] = L[Lo + sz - 1];
+    if (npair <= 0) return;
+    const double2* L2 = reinterpret_cast<const double2*>(L + Lo + head);
+    constexpr int B = 16;
+    for (int t0 = 0; t0 < npair; t0 += B * 64) {
+        double2 v[B];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) v[q] = L[Lo + t + q * 64];
+        for (int q = 0; q < B; ++q) {
+            const int t = t0 + q * 64 + lane;
+            v[q] = L2[t < npair ? t : npair - 1];  // clamped: branch-free, every load in flight
+        }
 #pragma unroll
-        for (int q = 0; q < 8; ++q) P[t + q * 64] = v[q];
+        for (int q = 0; q < B; ++q) {
+            const int t = t0 + q * 64 + lane;
+            if (t < npair) {
+                P[head + 2 * t] = v[q].x;
+                P[head + 2 * t + 1] = v[q].y;
+            }
+        }
     }
-    for (; t < sz; t += 64) P[t] = L[Lo + t];
 }
 
-__global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* __restrict__ fronts) {
-    // Latency-bound per front: the global loads are grouped into three dependent round trips
-    // {front record} -> {row ids, pivoted positions, pivot kinds, children's edge records, L panel}
-    // -> {w at the pivot rows, children's update vectors and maps (CH children in flight at once)};
-    // everything after that runs from LDS and registers.
-    extern __shared__ __attribute__((aligned(16))) double smem_s[];
-    const int f = fronts[blockIdx.x];
-    const int m = A.fm[f], p = A.fp[f];
-    const int lane = threadIdx.x;
-    const int64_t ro = A.rows_off[f];
-    const int64_t Lo = A.L_off[f];
-    const int c0 = A.child_off[f], c1 = A.child_off[f + 1];
-    const int sz = p * m - p * (p - 1) / 2;
-    double* P = smem_s;
-    double* y = smem_s + ((sz + 1) & ~1);
-    int32_t* fpl = (int32_t*)(y + ((m + 1) & ~1));  // this front's rows were permuted by pivoting
-    // round trip 2 (m <= kMaxLdsFront = 2 * 64 rows per lane)
-    const int mypiv = lane < p ? (int)A.piv[ro + lane] : 0;
-    int32_t fr0 = 0, fr1 = 0;
-    if (lane < p) fr0 = A.frow[ro + lane];
-    if (lane + 64 < p) fr1 = A.frow[ro + lane + 64];
-    const int32_t fp0 = lane < m ? A.fpos[ro + lane] : 0;
-    const int32_t fp1 = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
-    int my_cm = 0;
-    long long my_rmo = 0;
-    if (lane < c1 - c0) {
-        my_cm = A.ch_cm[c0 + lane];
-        my_rmo = A.ch_relmap_off[c0 + lane];
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return as_double(__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((unsigned long long*)p, as_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kDfSpinLimit = 1 << 22;  // polls (each behind s_sleep 2): about a second
+
+// Poll *addr (sc1) until it reaches `target` (wrap-safe); false on abort / limit.  Wave-uniform.
+__device__ __noinline__ bool df_wait(const uint32_t* addr, uint32_t target, uint32_t* abort_flag) {
+    uint32_t v = ld_sc1_u32(addr);
+    int it = 0;
+    while ((int32_t)(v - target) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        v = ld_sc1_u32(addr);
+        if ((++it & 63) == 0) {
+            if (ld_sc1_u32(abort_flag)) return false;
+            if (it >= kDfSpinLimit) {
+                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+        }
     }
-    stage_panel(A.L, Lo, sz, P);
-    // round trip 3
-    if (lane < m) { y[lane] = lane < p ? A.w[fr0] : 0.0; fpl[lane] = fp0; }
-    if (lane + 64 < m) { y[lane + 64] = lane + 64 < p ? A.w[fr1] : 0.0; fpl[lane + 64] = fp1; }
-    __syncthreads();
+    return true;
+}
+
+// every store of this wave has completed (sc1 stores: written through) before the signal below
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ---- per-front pieces shared by both schedules ----
+
+// children's update vectors -> y (LDS rows, permuted by fpl); CH children's loads in flight at once
+template <bool DF>
+__device__ __forceinline__ void fwd_extend_add(const SolveArgs& A, const DfArgs& D, int c0, int c1, int my_cm,
+                                               long long my_rmo, long long my_cxo, double* y, const int32_t* fpl) {
+    const int lane = threadIdx.x;
     constexpr int CH = 4;
     for (int cb = c0; cb < c1; cb += CH) {
         if (cb != c0 && (cb - c0) % 64 == 0 && lane < c1 - cb) {  // more than 64 children: next records
             my_cm = A.ch_cm[cb + lane];
             my_rmo = A.ch_relmap_off[cb + lane];
+            if (DF) my_cxo = D.ch_cvx_off[cb + lane];
         }
         double v[CH][2];
         int32_t r[CH][2];
@@ -1300,10 +1340,12 @@ __global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* 
             const bool have = cb + u < c1;  // uniform
             const int cm = have ? __builtin_amdgcn_readlane(my_cm, q) : 0;
             const int64_t off = have ? (int64_t)readlane64((unsigned long long)my_rmo, q) : 0;
+            const int64_t offx = DF && have ? (int64_t)readlane64((unsigned long long)my_cxo, q) : 0;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int t = lane + 64 * h;
-                v[u][h] = t < cm ? A.cvec[off + t] : 0.0;
+                if (DF) v[u][h] = t < cm ? ld_sc1(D.cvx + offx + t) : 0.0;
+                else v[u][h] = t < cm ? A.cvec[off + t] : 0.0;
                 r[u][h] = t < cm ? A.relmap[off + t] : -1;
             }
         }
@@ -1313,35 +1355,52 @@ __global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* 
             for (int h = 0; h < 2; ++h)
                 if (r[u][h] >= 0) y[fpl[r[u][h]]] += v[u][h];
     }
-    __syncthreads();
-    // triangle
-    double yi = lane < p ? y[lane] : 0.0;
+}
+
+// LDS readable beyond a front's panel + rows by the unclamped operand reads of fwd/bwd_compute
+constexpr int kSolveSlack = 192;  // doubles (>= p + 128 for p <= 64)
+
+// Forward elimination of one front from LDS (panel P = packed columns, rows y), one pass over the
+// pivot columns: y_k is final when step k starts, so each step updates the triangle rows (lane i owns
+// y_i, i < p) AND the contribution rows (lane i owns rows p + i and p + 64 + i): one readlane
+// broadcast of y_k, two or three LDS operand reads (unclamped, see kSolveSlack), two or three FMAs.
+// A 2x2 pivot (k, k+1) acts as two column steps on the rows below it; a null pivot adds nothing.
+template <bool DF>
+__device__ __forceinline__ void fwd_compute(int m, int p, const double* P, double* y, int mypiv, double* zdst,
+                                            double* cvo) {
+    const int lane = threadIdx.x;
+    const bool tri = lane < p;
+    const bool two = m - p > 64;  // uniform
+    double yi = tri ? y[lane] : 0.0;
+    double a0 = p + lane < m ? y[p + lane] : 0.0;
+    double a1 = two && p + 64 + lane < m ? y[p + 64 + lane] : 0.0;
+    const double* pt = P + lane;      // pt[pc] = L(lane, k), pc = start of column k
+    const double* pr = P + p + lane;  // pr[pc] = L(p + lane, k), pr[pc + 64] = L(p + 64 + lane, k)
+    int pc = 0;
     for (int k = 0; k < p; ++k) {
+        const double lt = pt[pc], l0 = pr[pc];
+        const double l1 = two ? pr[pc + 64] : 0.0;
         const int kind = __builtin_amdgcn_readlane(mypiv, k);
-        if (kind == PIV_1X1) {
-            const double yk = readlane_d(yi, k);
-            if (lane > k && lane < p) yi -= P[pcol(m, k) + lane] * yk;
-        } else if (kind == PIV_2X2_A) {
-            const double y0 = readlane_d(yi, k), y1 = readlane_d(yi, k + 1);
-            if (lane > k + 1 && lane < p) yi -= P[pcol(m, k) + lane] * y0 + P[pcol(m, k + 1) + lane] * y1;
-            ++k;
-        }
+        const bool live = kind == PIV_1X1 || kind == PIV_2X2_A || kind == PIV_2X2_B;
+        const double yk = live ? readlane_d(yi, k) : 0.0;
+        const int lim = kind == PIV_2X2_A ? k + 1 : k;
+        const double t = yi - lt * yk;
+        yi = (tri && lane > lim) ? t : yi;
+        a0 -= l0 * yk;
+        a1 -= l1 * yk;
+        pc += m - k - 1;
     }
-    if (lane < p) y[lane] = yi;
-    __syncthreads();
-    // rectangle: contribution rows, handed to the parent
-    double* cvo = A.cvec + A.relmap_off[f];
-    for (int i = p + lane; i < m; i += 64) {
-        double acc = y[i];
-        int pc = 0;
-        for (int k = 0; k < p; ++k) {
-            acc -= P[pc + i] * y[k];
-            pc += m - k - 1;
-        }
-        cvo[i - p] = acc;
+    if (p + lane < m) {
+        if (DF) st_sc1(cvo + lane, a0);
+        else cvo[lane] = a0;
     }
-    // block diagonal
-    if (lane < p) {
+    if (two && p + 64 + lane < m) {
+        if (DF) st_sc1(cvo + 64 + lane, a1);
+        else cvo[64 + lane] = a1;
+    }
+    if (tri) y[lane] = yi;
+    __syncthreads();  // y of the 2x2 partners below
+    if (tri) {
         const int kind = mypiv;
         double out = 0.0;  // null pivot contributes 0
         if (kind == PIV_1X1) {
@@ -1354,8 +1413,72 @@ __global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* 
             const double y0 = y[k0], y1 = y[k0 + 1];
             out = kind == PIV_2X2_A ? (e * y0 - b * y1) / det : (a * y1 - b * y0) / det;
         }
-        A.w[fr0] = out;
+        *zdst = out;
     }
+}
+
+// Backward substitution of one front from LDS (panel P, x: own pivots z, contribution rows final):
+// returns x_j in lane j < p.  Rectangle: lane k dots column k with the broadcast contribution rows;
+// triangle: steps k = p-1 .. 0, x_k broadcast by readlane, operand L(k, lane) read unclamped.
+__device__ __forceinline__ double bwd_compute(int m, int p, const double* P, const double* x, int mypiv) {
+    const int lane = threadIdx.x;
+    const bool tri = lane < p;
+    const double* pk = P + pcol(m, tri ? lane : 0);  // pk[i] = L(i, lane), i >= lane
+    double s0 = 0.0, s1 = 0.0;
+    int i = p;
+    for (; i + 1 < m; i += 2) {
+        s0 += pk[i] * x[i];
+        s1 += pk[i + 1] * x[i + 1];
+    }
+    if (i < m) s0 += pk[i] * x[i];
+    const bool live = tri && mypiv != PIV_NULL;
+    double xj = tri ? x[lane] : 0.0;
+    if (live) xj -= s0 + s1;
+    for (int k = p - 1; k >= 0; --k) {
+        const double l = pk[k];  // L(k, lane) for lane < k (other lanes read in-bounds garbage)
+        const int kind = __builtin_amdgcn_readlane(mypiv, k);
+        const double xk = kind != PIV_NULL ? readlane_d(xj, k) : 0.0;
+        const int skip = kind == PIV_2X2_B ? k - 1 : -1;
+        const double t = xj - l * xk;
+        xj = (live && lane < k && lane != skip) ? t : xj;
+    }
+    return xj;
+}
+
+// ---- level-synchronous schedule: one block per front ----
+__global__ __launch_bounds__(64) void k_solve_fwd_w(SolveArgs A, const int32_t* __restrict__ fronts) {
+    // Latency-bound per front: the global loads are grouped into three dependent round trips
+    // {front record} -> {row ids, pivoted positions, pivot kinds, children's edge records, L panel}
+    // -> {w at the pivot rows, children's update vectors and maps}; the rest runs from LDS/registers.
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int lane = threadIdx.x;
+    const int64_t ro = A.rows_off[f];
+    const int c0 = A.child_off[f], c1 = A.child_off[f + 1];
+    const int sz = p * m - p * (p - 1) / 2;
+    double* P = smem_s;
+    double* y = smem_s + ((sz + 1) & ~1);
+    int32_t* fpl = (int32_t*)(y + ((m + 1) & ~1));  // this front's rows were permuted by pivoting
+    const int mypiv = lane < p ? (int)A.piv[ro + lane] : 0;
+    int32_t fr0 = 0, fr1 = 0;
+    if (lane < p) fr0 = A.frow[ro + lane];
+    if (lane + 64 < p) fr1 = A.frow[ro + lane + 64];
+    const int32_t fp0 = lane < m ? A.fpos[ro + lane] : 0;
+    const int32_t fp1 = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
+    int my_cm = 0;
+    long long my_rmo = 0;
+    if (lane < c1 - c0) {
+        my_cm = A.ch_cm[c0 + lane];
+        my_rmo = A.ch_relmap_off[c0 + lane];
+    }
+    stage_panel(A.L, A.L_off[f], sz, P);
+    if (lane < m) { y[lane] = lane < p ? A.w[fr0] : 0.0; fpl[lane] = fp0; }
+    if (lane + 64 < m) { y[lane + 64] = lane + 64 < p ? A.w[fr1] : 0.0; fpl[lane + 64] = fp1; }
+    __syncthreads();
+    fwd_extend_add<false>(A, DfArgs{}, c0, c1, my_cm, my_rmo, 0, y, fpl);
+    __syncthreads();
+    fwd_compute<false>(m, p, P, y, mypiv, A.w + fr0, A.cvec + A.relmap_off[f]);
 }
 
 __global__ __launch_bounds__(64) void k_solve_bwd_w(SolveArgs A, const int32_t* __restrict__ fronts) {
@@ -1371,29 +1494,221 @@ __global__ __launch_bounds__(64) void k_solve_bwd_w(SolveArgs A, const int32_t* 
     for (int i = lane; i < m; i += 64) x[i] = A.w[A.frow[ro + i]];
     stage_panel(A.L, A.L_off[f], sz, P);
     __syncthreads();
-    // rectangle: lane k accumulates sum_{i>=p} L(i,k) x_i (x_i broadcast from LDS)
-    double xj = 0.0;
-    if (lane < p) {
-        const double* Pk = P + pcol(m, lane);
-        double s0 = 0.0, s1 = 0.0;
-        int i = p;
-        for (; i + 1 < m; i += 2) {
-            s0 += Pk[i] * x[i];
-            s1 += Pk[i + 1] * x[i + 1];
-        }
-        if (i < m) s0 += Pk[i] * x[i];
-        xj = x[lane];
-        if (mypiv != PIV_NULL) xj -= s0 + s1;
-    }
-    // triangle (transposed): lane j owns x_j
-    for (int k = p - 1; k >= 0; --k) {
-        const int kind = __builtin_amdgcn_readlane(mypiv, k);
-        if (kind == PIV_NULL) continue;
-        const double xk = readlane_d(xj, k);
-        const int skip = kind == PIV_2X2_B ? k - 1 : -1;
-        if (lane < k && lane != skip && mypiv != PIV_NULL) xj -= P[pcol(m, lane) + k] * xk;
-    }
+    const double xj = bwd_compute(m, p, P, x, mypiv);
     if (lane < p) A.w[A.frow[ro + lane]] = xj;
+}
+
+// ---- dataflow schedule: a resident grid walks the topological order, software-pipelined ----
+// Per block, fronts t, t + grid, ...: while front t computes, the next front's record (scalar),
+// row data, dependency word and (up to kPre * 128 doubles of) L panel are in flight into registers,
+// including its own-pivot values: the dataflow solve works on xs, the solution vector in elimination
+// order (each front's pivots contiguous in a 128-byte-aligned slot; right-hand side scattered in and
+// solution gathered out by k_xs_in / k_xs_out), so a front's own values need no row-id round trip.
+// A front then costs one dependent round trip (its children's / ancestors' values), its arithmetic
+// and the store drain before its signal.
+constexpr int kPre = 16;
+struct FrontRec {
+    int f, m, p, sz, par, c0, c1;
+    int64_t ro, Lo;
+    int64_t xoff;  // forward: cvx slot
+    int64_t woff;  // xs slot (the front's pivots in elimination order)
+};
+struct FrontPre {
+    FrontRec r;
+    int head, npair;
+    int mypiv;
+    int32_t a0, a1;    // backward: xs index (rxpos) of the contribution rows lane, lane + 64 (>= p)
+    int32_t fp0, fp1;  // forward: pivoted positions of the analysis-order rows
+    int my_cm;
+    long long my_rmo, my_cxo;
+    uint32_t dep;      // dependency word as loaded at prefetch time (sc1)
+    double e0;         // xs at the own pivots (forward: scaled right-hand side; backward: z)
+    double hv, tv;     // panel elements outside the 16-byte pairs (leading / trailing double)
+    double2 v[kPre];
+};
+
+template <bool FWD>
+__device__ __forceinline__ FrontRec df_record(const SolveArgs& A, const DfArgs& D, int f) {
+    FrontRec r;
+    r.f = f;
+    r.m = A.fm[f];
+    r.p = A.fp[f];
+    r.ro = A.rows_off[f];
+    r.Lo = A.L_off[f];
+    r.par = D.parent[f];
+    r.c0 = FWD ? A.child_off[f] : 0;
+    r.c1 = FWD ? A.child_off[f + 1] : 0;
+    r.xoff = FWD ? D.cvx_off[f] : 0;
+    r.woff = D.xs_off[f];
+    r.sz = r.p * r.m - r.p * (r.p - 1) / 2;
+    return r;
+}
+
+template <bool FWD>
+__device__ __forceinline__ void df_issue(const SolveArgs& A, const DfArgs& D, FrontPre& q) {
+    const int lane = threadIdx.x;
+    const int m = q.r.m, p = q.r.p;
+    const int64_t ro = q.r.ro;
+    q.mypiv = lane < p ? (int)A.piv[ro + lane] : (FWD ? 0 : (int)PIV_NULL);
+    q.my_cm = 0;
+    q.my_rmo = q.my_cxo = 0;
+    q.fp0 = q.fp1 = 0;
+    q.e0 = lane < p ? D.xs[q.r.woff + lane] : 0.0;
+    if (FWD) {
+        q.a0 = q.a1 = 0;
+        q.fp0 = lane < m ? A.fpos[ro + lane] : 0;
+        q.fp1 = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
+        if (lane < q.r.c1 - q.r.c0) {
+            q.my_cm = A.ch_cm[q.r.c0 + lane];
+            q.my_rmo = A.ch_relmap_off[q.r.c0 + lane];
+            q.my_cxo = D.ch_cvx_off[q.r.c0 + lane];
+        }
+        q.dep = q.r.c1 > q.r.c0 ? ld_sc1_u32(D.cnt + q.r.f) : 0u;
+    } else {
+        q.a0 = lane < m && lane >= p ? D.rxpos[ro + lane] : 0;
+        q.a1 = lane + 64 < m && lane + 64 >= p ? D.rxpos[ro + lane + 64] : 0;
+        q.dep = q.r.par >= 0 ? ld_sc1_u32(D.done + q.r.par) : 0u;
+    }
+    q.head = (int)(q.r.Lo & 1) < q.r.sz ? (int)(q.r.Lo & 1) : q.r.sz;
+    q.npair = (q.r.sz - q.head) >> 1;
+    const double2* L2 = reinterpret_cast<const double2*>(A.L + q.r.Lo + q.head);
+    const int last = q.npair > 0 ? q.npair - 1 : 0;
+    q.hv = q.head ? A.L[q.r.Lo] : 0.0;
+    q.tv = ((q.r.sz - q.head) & 1) ? A.L[q.r.Lo + q.r.sz - 1] : 0.0;
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const int t = u * 64 + lane;
+        q.v[u] = q.npair > 0 ? L2[t < q.npair ? t : last] : make_double2(0.0, 0.0);
+    }
+}
+
+// prefetched panel -> LDS (plus the rare remainder beyond the prefetch, loaded here)
+__device__ __forceinline__ void df_stage(const SolveArgs& A, const FrontPre& q, double* P) {
+    const int lane = threadIdx.x;
+    if (q.head && lane == 0) P[0] = q.hv;
+    if (((q.r.sz - q.head) & 1) && lane == 0) P[q.r.sz - 1] = q.tv;
+#pragma unroll
+    for (int u = 0; u < kPre; ++u) {
+        const int t = u * 64 + lane;
+        if (t < q.npair) {
+            P[q.head + 2 * t] = q.v[u].x;
+            P[q.head + 2 * t + 1] = q.v[u].y;
+        }
+    }
+    if (q.npair > kPre * 64) {
+        const double2* L2 = reinterpret_cast<const double2*>(A.L + q.r.Lo + q.head);
+        for (int t = kPre * 64 + lane; t < q.npair; t += 64) {
+            const double2 v = L2[t];
+            P[q.head + 2 * t] = v.x;
+            P[q.head + 2 * t + 1] = v.y;
+        }
+    }
+}
+
+// The walk keeps ONE FrontPre: once a front's prefetched data is consumed (staged into LDS, its
+// scalars copied), the next front's loads are issued into the same registers, so no register copy of
+// an in-flight load (which would wait for it) is needed across iterations.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_solve_fwd_df(SolveArgs A, DfArgs D) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    int t = blockIdx.x;
+    if (t >= D.nf) return;
+    FrontPre q;
+    q.r = df_record<true>(A, D, D.order[t]);
+    df_issue<true>(A, D, q);
+    for (; t < D.nf; t += gridDim.x) {
+        // next position (clamped: the last front re-prefetches itself, branch-free loop-carried loads)
+        const int tn = min(t + (int)gridDim.x, D.nf - 1);
+        const FrontRec rn = df_record<true>(A, D, D.order[tn]);  // used after the children's loads
+        const int m = q.r.m, p = q.r.p, f = q.r.f, par = q.r.par, mypiv = q.mypiv;
+        const int64_t xoff = q.r.xoff, woff = q.r.woff;
+        unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f : nullptr;
+        if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+        double* P = smem_s;
+        double* y = smem_s + ((q.r.sz + 1) & ~1);
+        int32_t* fpl = (int32_t*)(y + ((m + 1) & ~1));  // this front's rows were permuted by pivoting
+        if (lane < m) { y[lane] = q.e0; fpl[lane] = q.fp0; }
+        if (lane + 64 < m) { y[lane + 64] = 0.0; fpl[lane + 64] = q.fp1; }
+        const uint32_t target = D.epoch * (uint32_t)(q.r.c1 - q.r.c0);
+        if ((int32_t)(q.dep - target) < 0) df_wait(D.cnt + f, target, D.abort_flag);
+        df_stage(A, q, P);
+        __syncthreads();
+        fwd_extend_add<true>(A, D, q.r.c0, q.r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
+        __syncthreads();
+        if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+        q.r = rn;
+        df_issue<true>(A, D, q);
+        if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+        fwd_compute<true>(m, p, P, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
+        if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+        drain_stores();
+        if (par >= 0 && lane == 0) __hip_atomic_fetch_add(D.cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();  // LDS reused by the next front
+    }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_solve_bwd_df(SolveArgs A, DfArgs D) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    int t = blockIdx.x;
+    if (t >= D.nf) return;
+    FrontPre q;
+    q.r = df_record<false>(A, D, D.order[D.nf - 1 - t]);
+    df_issue<false>(A, D, q);
+    for (; t < D.nf; t += gridDim.x) {
+        const int tn = min(t + (int)gridDim.x, D.nf - 1);
+        const FrontRec rn = df_record<false>(A, D, D.order[D.nf - 1 - tn]);
+        const int m = q.r.m, p = q.r.p, f = q.r.f, mypiv = q.mypiv;
+        const int64_t woff = q.r.woff;
+        unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f + 4 : nullptr;
+        if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+        double* P = smem_s;
+        double* x = smem_s + ((q.r.sz + 1) & ~1);
+        // own pivots: z of the forward solve; contribution rows: the ancestors' published solution
+        // values (this launch), through the per-row slot index rxpos, once the parent has published
+        if (q.r.par >= 0 && (int32_t)(q.dep - D.epoch) < 0) df_wait(D.done + q.r.par, D.epoch, D.abort_flag);
+        if (lane < m) x[lane] = lane < p ? q.e0 : ld_sc1(D.xs + q.a0);
+        if (lane + 64 < m) x[lane + 64] = ld_sc1(D.xs + q.a1);
+        df_stage(A, q, P);
+        __syncthreads();
+        if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+        q.r = rn;
+        df_issue<false>(A, D, q);
+        if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+        const double xj = bwd_compute(m, p, P, x, mypiv);
+        if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+        if (lane < p) st_sc1(D.xs + woff + lane, xj);
+        drain_stores();
+        if (lane == 0) __hip_atomic_store(D.done + f, D.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();
+    }
+}
+
+// right-hand side into elimination order (xs[xpos[i]] = s_i b_i) and the solution back (x_i = s_i xs[xpos[i]])
+__global__ void k_xs_in(const double* __restrict__ b, const double* __restrict__ scale, const int32_t* __restrict__ xpos,
+                        double* __restrict__ xs, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        xs[xpos[i]] = scale[i] * b[i];
+}
+__global__ void k_xs_out(const double* __restrict__ xs, const double* __restrict__ scale, const int32_t* __restrict__ xpos,
+                         double* __restrict__ x, int64_t n) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        x[i] = scale[i] * xs[xpos[i]];
+}
+
+// Per-factorization map for the dataflow backward solve: rxpos[row slot] = xs index of the row's
+// solution value (pass 0: xpos[original id] of every pivot; pass 1: rows >= p of every front).
+__global__ __launch_bounds__(64) void k_xpos(SolveArgs A, DfArgs D, int32_t* __restrict__ xpos, int32_t* __restrict__ rxpos,
+                                             int pass) {
+    for (int f = blockIdx.x; f < D.nf; f += gridDim.x) {
+        const int m = A.fm[f], p = A.fp[f];
+        const int64_t ro = A.rows_off[f];
+        if (pass == 0) {
+            for (int i = threadIdx.x; i < p; i += 64) xpos[A.frow[ro + i]] = (int32_t)(D.xs_off[f] + i);
+        } else {
+            for (int i = p + threadIdx.x; i < m; i += 64) rxpos[ro + i] = xpos[A.frow[ro + i]];
+        }
+    }
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1589,9 +1904,52 @@ hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, in
 hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int count, int lds_doubles, bool forward,
                              hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    const size_t sh = (size_t)lds_doubles * sizeof(double) + 16;
+    const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;
     if (forward) hipLaunchKernelGGL(k_solve_fwd_w, dim3(count), dim3(64), sh, s, A, fronts);
     else hipLaunchKernelGGL(k_solve_bwd_w, dim3(count), dim3(64), sh, s, A, fronts);
+    return hipGetLastError();
+}
+
+int solve_df_grid(int lds_doubles, int nf) {
+    const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;
+    int dev = 0, cus = 0, nf_blk = 0, nb_blk = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nf_blk, k_solve_fwd_df, 64, sh) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_blk, k_solve_bwd_df, 64, sh) != hipSuccess) return 0;
+    // one block per CU below the reported residency (the query can over-report by one)
+    int per_cu = std::min(nf_blk, nb_blk) - 1;
+    if (getenv("UNO_KKT_DF_DEBUG")) fprintf(stderr, "[uno_kkt] df occupancy fwd %d bwd %d per CU, %d CUs, lds %zu B\n", nf_blk, nb_blk, cus, sh);
+    if (per_cu < 1) return 0;
+    const int64_t g = (int64_t)per_cu * cus;
+    return (int)std::min<int64_t>(g, std::max(nf, 1));
+}
+
+hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s) {
+    if (D.nf <= 0 || grid <= 0) return hipSuccess;
+    const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;
+    if (forward) hipLaunchKernelGGL(k_solve_fwd_df, dim3(grid), dim3(64), sh, s, A, D);
+    else hipLaunchKernelGGL(k_solve_bwd_df, dim3(grid), dim3(64), sh, s, A, D);
+    return hipGetLastError();
+}
+
+hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_xs_in, dim3(grid_for(n, 256)), dim3(256), 0, s, b, scale, xpos, xs, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, double* x, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, x, n);
+    return hipGetLastError();
+}
+
+hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, hipStream_t s) {
+    if (D.nf <= 0) return hipSuccess;
+    const int g = std::min(D.nf, 8192);
+    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(64), 0, s, A, D, xpos, rxpos, 0);
+    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(64), 0, s, A, D, xpos, rxpos, 1);
     return hipGetLastError();
 }
 

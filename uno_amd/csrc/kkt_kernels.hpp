@@ -66,6 +66,25 @@ struct SolveArgs {
     const int64_t* ch_relmap_off;  // per child edge: offset into relmap / cvec
 };
 
+// Dataflow (one launch per direction) solve schedule, kkt_kernels.hip k_solve_fwd_df / k_solve_bwd_df
+struct DfArgs {
+    const int32_t* order;       // fronts, children before parents (the backward solve walks it from the end)
+    int32_t nf;
+    const int32_t* parent;      // assembly-tree parent (-1 = root)
+    uint32_t* cnt;              // forward: children arrived; epoch * children once all have (cumulative)
+    uint32_t* done;             // backward: epoch of the front's last published solution
+    uint32_t epoch;             // 1, 2, ... per solve since the counters were cleared
+    double* cvx;                // forward update vectors, one 128-byte-aligned slot per front
+    const int64_t* cvx_off;     // per front
+    const int64_t* ch_cvx_off;  // per child edge (aligned with child)
+    double* xs;                 // solution vector in elimination order: each front's pivots in a 128-byte-aligned slot
+    const int64_t* xs_off;      // per front
+    const int32_t* rxpos;       // per front row (layout of frow): xs index of the rows >= p
+    uint32_t* abort_flag;       // set when a wait exceeded its limit (result invalid, host falls back)
+    unsigned long long* stamps; // diagnostics (nullptr in normal runs): per front and direction 4 s_memrealtime
+                                // words {start, dependency satisfied, values staged, published}
+};
+
 // row-wise scans for the equilibration and ||A_pre||_inf (kkt_kernels.hip k_rowscan)
 struct ScanArgs {
     int64_t n;               // rows to scan (list entries, or rows 0..n-1 when list is null)
@@ -129,6 +148,15 @@ hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
                         hipStream_t s);
+
+// dataflow solve: one resident grid of one-wave blocks per direction (grid from the occupancy query)
+int solve_df_grid(int lds_doubles, int nf);
+hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
+// rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch
+hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, hipStream_t s);
+// xs[xpos[i]] = scale_i b_i  /  x_i = scale_i xs[xpos[i]]
+hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s);
+hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, double* x, int64_t n, hipStream_t s);
 
 constexpr int kMaxLdsFront = 128;     // fronts up to this order factor entirely in LDS
 constexpr int kMaxGlobalFront = 8192; // larger fronts are rejected at analysis

@@ -31,7 +31,8 @@ class KKTStats(ctypes.Structure):
         ("n_dense", ctypes.c_int64), ("pivots_2x2", ctypes.c_int64), ("pivots_null", ctypes.c_int64),
         ("pivots_relaxed", ctypes.c_int64), ("factorizations", ctypes.c_int64), ("solves", ctypes.c_int64),
         ("flops", ctypes.c_double), ("analysis_seconds", ctypes.c_double), ("bytes_L", ctypes.c_double),
-        ("bytes_cb", ctypes.c_double), ("fronts_merged", ctypes.c_int64),
+        ("bytes_cb", ctypes.c_double), ("fronts_merged", ctypes.c_int64), ("solve_grid", ctypes.c_int64),
+        ("solve_aborts", ctypes.c_int64),
     ]
 
     def as_dict(self):
