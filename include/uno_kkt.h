@@ -54,6 +54,8 @@ typedef struct {
     int64_t fronts_merged;  /* fronts amalgamated into their parent since analysis (delayed pivots) */
     int64_t solve_grid;     /* dataflow solve: resident one-wave blocks per direction (0 = level-scheduled) */
     int64_t solve_aborts;   /* dataflow solves abandoned at the dependency-wait limit (then level-scheduled) */
+    int64_t factor_df_fronts; /* fronts factored by the one-launch dataflow kernel (upper tree; 0 = none) */
+    int64_t factor_df_aborts; /* dataflow factorizations redone level by level after a wait limit */
 } uno_kkt_stats_t;
 
 /* Create a solver bound to HIP device `device_id`.  Replaces MUMPS JOB=-1 (MUMPSSolver.cpp:16-37). */

@@ -183,17 +183,21 @@ def test_empty_and_tiny(uno_amd):
 
 
 @pytest.mark.parametrize("n", [10000, 200000])
-def test_dataflow_solve_matches_level_schedule(uno_amd, n):
-    """The one-launch dataflow solve (k_solve_*_df: fronts wait on arrival counters inside the launch)
-    does the same arithmetic as the level-scheduled launches: solutions bit-identical, over repeated
-    solves (cumulative epoch counters) and after a refactorization with other values (new pivoting)."""
+def test_dataflow_matches_level_schedule(uno_amd, n):
+    """The one-launch dataflow factorization of the upper tree (k_factor_df) and dataflow solves
+    (k_solve_*_df: fronts wait on arrival counters inside the launch) do the same arithmetic as the
+    level-scheduled launches: inertia equal and solutions bit-identical, over repeated solves
+    (cumulative epoch counters) and after a refactorization with other values (new pivoting)."""
     from uno_amd import HipKKT, arrowband, SEEDS
     N, nv, m, r, c, v, b = arrowband(n, SEEDS["C2"])
-    gd, gl = HipKKT(0), HipKKT(0, dataflow_solve=0)
+    gd, gl = HipKKT(0), HipKKT(0, dataflow_solve=0, dataflow_factor=0)
     for g in (gd, gl):
         g.analyze(N, r, c)
         g.factorize(v)
-    assert gd.stats()["solve_grid"] > 0 and gl.stats()["solve_grid"] == 0
+    assert gd.inertia() == gl.inertia()
+    sd, sl = gd.stats(), gl.stats()
+    assert sd["solve_grid"] > 0 and sl["solve_grid"] == 0
+    assert sd["factor_df_fronts"] > 0 and sl["factor_df_fronts"] == 0
     xl = gl.solve(b)
     for rep in range(3):
         xd = gd.solve(b * (rep + 1))
@@ -207,4 +211,4 @@ def test_dataflow_solve_matches_level_schedule(uno_amd, n):
     assert gd.inertia() == gl.inertia()
     b2 = np.cos(np.arange(N))
     np.testing.assert_array_equal(gd.solve(b2), gl.solve(b2))
-    assert gd.stats()["solve_aborts"] == 0
+    assert gd.stats()["solve_aborts"] == 0 and gd.stats()["factor_df_aborts"] == 0

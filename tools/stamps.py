@@ -58,3 +58,8 @@ for lev in range(fl.max() + 1):
           f"update {(cu[s]/steps[s]).mean():7.0f} rest {(cr[s]/steps[s]).mean():6.0f} | span {(st[s,3].max()-st[s,0].min())*10e-3:8.1f} us")
 tot = sum((st[fl == l, 3].max() - st[fl == l, 0].min()) * 10e-3 for l in range(fl.max() + 1))
 print(f"sum of level spans {tot:.1f} us")
+t0 = st[:, 0].min()
+print("timeline (us from the first front start): level first start .. last end")
+for lev in range(fl.max() + 1):
+    s = fl == lev
+    print(f"  level {lev:2d} {(st[s, 0].min() - t0) * 10e-3:8.1f} .. {(st[s, 3].max() - t0) * 10e-3:8.1f}")

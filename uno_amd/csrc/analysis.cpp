@@ -330,7 +330,9 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
         S.f_rows_off[b + 1] = S.f_rows_off[b] + m;
         S.f_L_off[b + 1] = S.f_L_off[b] + p * m - p * (p - 1) / 2;
         int64_t cm = m - p;
-        S.f_cb_off[b + 1] = S.f_cb_off[b] + cm * (cm + 1) / 2;
+        // 128-byte-aligned blocks: no cache line holds two fronts' contribution blocks (the dataflow
+        // factorization hands them over inside one launch, kkt_kernels.hip k_factor_df)
+        S.f_cb_off[b + 1] = (S.f_cb_off[b] + cm * (cm + 1) / 2 + 15) & ~(int64_t)15;
         S.nnz_L += p * (m - p) + p * (p - 1) / 2;
         for (int64_t k = 0; k < p; ++k) {
             double r = (double)(m - k - 1);

@@ -55,6 +55,7 @@ const char* kClassNames[KC_COUNT] = {"pack", "scale", "factor_lds", "factor_glob
 struct Launch {
     int begin, count, mmax;
     bool global;
+    int level;
 };
 
 // one solve launch: fronts solve_fronts[begin, begin+count) of one level; wave kernels (p <= 64,
@@ -147,6 +148,15 @@ struct uno_kkt {
     DBuf<double> df_cvx, df_xs;
     int want_solve_stamps = 0;
     DBuf<unsigned long long> df_stamps;
+    // dataflow factorization of the upper tree (levels >= dff_level, every front one-wave); option
+    // "dataflow_factor" (default 1)
+    int dff_enabled = 1;
+    int dff_level = INT32_MAX;     // first level of the dataflow launch (INT32_MAX: none)
+    int dff_grid = 0, dff_mmax = 0;
+    uint32_t dff_epoch = 0;
+    int64_t dff_aborts = 0;
+    DBuf<int32_t> dff_order, dff_nch;
+    DBuf<uint32_t> dff_cnt;
     // distributed factorization (null comm: one GPU)
     // device-side vector work around the solve
     int64_t rhs_n = -1, rhs_m = -1;
@@ -341,7 +351,7 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
                     floor_ = prev_cap(floor_);
                 }
             }
-            P.fac.push_back({base + q, r - q, m0, global});
+            P.fac.push_back({base + q, r - q, m0, global, l});
             q = r;
         }
     }
@@ -528,6 +538,21 @@ int allreduce_host(uno_kkt_t h, std::vector<unsigned long long>& v, RedOp op) {
 // accepted pivot is at or below the exact null-pivot threshold, else refactor with the exact one
 int sync_and_verify(uno_kkt_t h) {
     HIPCHK(h, hipStreamSynchronize(h->stream));
+    uint32_t ab = 0;
+    memcpy(&ab, h->h_counters + 11, sizeof(ab));
+    if (ab != 0) {
+        // a dependency wait of the dataflow factorization hit its limit: the factorization is invalid;
+        // level-scheduled launches from now on, and this one is redone
+        h->dff_aborts++;
+        h->dff_enabled = 0;
+        h->dff_level = INT32_MAX;
+        memset(h->h_counters + 11, 0, 8);
+        HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), h->stream));
+        if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow factorization aborted: refactoring level by level\n");
+        int rc = enqueue_factorization(h);
+        if (rc != UNO_KKT_OK) return rc;
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+    }
     if (h->last_optimistic) {
         HIPCHK(h, hipEventSynchronize(h->ev_norm));
         double anorm, mp;
@@ -634,11 +659,51 @@ int finish_factorization(uno_kkt_t h) {
 
 // Dataflow solve layout: topological front order (the level order), 128-byte-aligned per-front slots
 // for the forward update vectors and the backward solution values, arrival counters.
+hipError_t setup_factor_dataflow(uno_kkt_t h) {
+    const Symbolic& S = h->S;
+    h->dff_level = INT32_MAX;
+    h->dff_grid = 0;
+    h->dff_epoch = 0;
+    if (h->world > 1 || !h->dff_enabled || S.nf == 0) return hipSuccess;
+    // lowest level from which every front fits the one-wave register kernel (m <= 64)
+    int L = S.nlevels;
+    while (L > 0) {
+        bool ok = true;
+        for (int q = S.level_off[L - 1]; q < S.level_off[L] && ok; ++q) ok = S.f_m[S.level_fronts[q]] <= 64;
+        if (!ok) break;
+        --L;
+    }
+    if (L >= S.nlevels) return hipSuccess;
+    std::vector<int32_t> order(S.level_fronts.begin() + S.level_off[L], S.level_fronts.begin() + S.level_off[S.nlevels]);
+    std::vector<int32_t> nch(S.nf, 0);
+    int mmax = 1;
+    for (int32_t f : order) {
+        mmax = std::max(mmax, S.f_m[f]);
+        for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1]; ++q) nch[f] += S.f_level[S.child[q]] >= L;
+    }
+    hipStream_t s = h->stream;
+    hipError_t e;
+    if ((e = h->dff_order.upload(order, s)) != hipSuccess) return e;
+    if ((e = h->dff_nch.upload(nch, s)) != hipSuccess) return e;
+    if ((e = h->dff_cnt.alloc(S.nf)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(h->dff_cnt.p, 0, sizeof(uint32_t) * S.nf, s)) != hipSuccess) return e;
+    if (!h->df_abort.p && (e = h->df_abort.alloc(1)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
+    h->dff_mmax = mmax;
+    h->dff_grid = factor_df_grid(mmax, (int)order.size());
+    if (h->dff_grid > 0) h->dff_level = L;
+    if (h->verbose)
+        fprintf(stderr, "[uno_kkt] dataflow factorization: levels %d..%d, %zu fronts, grid %d\n", L, S.nlevels - 1,
+                order.size(), h->dff_grid);
+    return hipSuccess;
+}
+
 hipError_t setup_dataflow(uno_kkt_t h) {
     const Symbolic& S = h->S;
     h->df_grid = 0;
     h->df_rx_valid = false;
     h->df_epoch = 0;
+    if (hipError_t e = setup_factor_dataflow(h); e != hipSuccess) return e;
     if (h->world > 1 || !h->df_enabled || S.nf == 0) return hipSuccess;
     int lds = 0;
     for (int64_t f = 0; f < S.nf; ++f) {
@@ -870,9 +935,23 @@ int enqueue_factorization(uno_kkt_t h) {
         HIPCHK(h, hipMemsetAsync(h->stamps.p, 0, sizeof(unsigned long long) * 8 * S.nf, s));
         A.stamps = h->stamps.p;
     }
+    A.df_order = nullptr; A.df_nf = 0; A.df_nch = nullptr; A.df_cnt = nullptr; A.df_epoch = 0; A.df_abort = nullptr;
+    const bool dff = h->world == 1 && h->dff_level != INT32_MAX;
     for (const Launch& L : h->plan[0].fac) {
+        if (dff && L.level >= h->dff_level) continue;
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
         HIPCHK(h, launch_factor(A, h->plan[0].fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+    }
+    if (dff) {
+        TimerScope t(h, KC_FACTOR_LDS);
+        A.df_order = h->dff_order.p;
+        A.df_nf = (int32_t)h->dff_order.n;
+        A.df_nch = h->dff_nch.p;
+        A.df_cnt = h->dff_cnt.p;
+        A.df_epoch = ++h->dff_epoch;
+        A.df_abort = h->df_abort.p;
+        HIPCHK(h, launch_factor_df(A, h->dff_grid, h->dff_mmax, s));
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 11, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
     if (h->world > 1) {
         // subtree roots' contribution blocks -> rank 0 (same arena offsets on every rank)
@@ -959,6 +1038,13 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "verbose") h->verbose = (int)value;
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
+    else if (n == "dataflow_factor") {
+        h->dff_enabled = value != 0.0;
+        if (h->analyzed) {
+            HIPCHK(h, setup_factor_dataflow(h));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+    }
     else if (n == "dataflow_solve") {
         h->df_enabled = value != 0.0;
         if (h->analyzed) {
@@ -1200,6 +1286,8 @@ int uno_kkt_stats(uno_kkt_t h, uno_kkt_stats_t* out) {
     out->fronts_merged = h->merges_total;
     out->solve_grid = (h->world == 1 && h->df_enabled) ? h->df_grid : 0;
     out->solve_aborts = h->df_aborts;
+    out->factor_df_fronts = h->dff_level != INT32_MAX ? (int64_t)h->dff_order.n : 0;
+    out->factor_df_aborts = h->dff_aborts;
     return UNO_KKT_OK;
 }
 

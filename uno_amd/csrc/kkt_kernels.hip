@@ -207,6 +207,44 @@ __device__ __forceinline__ void tri_rc(int t, int& r, int& c) {
 }
 
 // ------------------------------------------------------------------------------------------------
+// inter-workgroup hand-offs of the dataflow schedules (factor: contribution blocks; solve: update
+// vectors and solution values): sc1 (write-through) stores, sc1 loads, one signalling lane after the
+// storing wave's vmcnt(0) (MI355X_MICROARCH.md, inter-workgroup visibility, first hand-off row)
+// ------------------------------------------------------------------------------------------------
+__device__ __forceinline__ double ld_sc1(const double* p) {
+    return as_double(__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+__device__ __forceinline__ void st_sc1(double* p, double v) {
+    __hip_atomic_store((unsigned long long*)p, as_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+constexpr int kDfSpinLimit = 1 << 22;  // polls (each behind s_sleep 2): about a second
+
+// Poll *addr (sc1) until it reaches `target` (wrap-safe); false on abort / limit.  Wave-uniform.
+__device__ __noinline__ bool df_wait(const uint32_t* addr, uint32_t target, uint32_t* abort_flag) {
+    uint32_t v = ld_sc1_u32(addr);
+    int it = 0;
+    while ((int32_t)(v - target) < 0) {
+        __builtin_amdgcn_s_sleep(2);
+        v = ld_sc1_u32(addr);
+        if ((++it & 63) == 0) {
+            if (ld_sc1_u32(abort_flag)) return false;
+            if (it >= kDfSpinLimit) {
+                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                return false;
+            }
+        }
+    }
+    return true;
+}
+
+// every store of this wave has completed (sc1 stores: written through) before the signal below
+__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// ------------------------------------------------------------------------------------------------
 // dense front factorization
 // ------------------------------------------------------------------------------------------------
 // Front storage: only the lower triangle A(i,j), j <= i, is kept.
@@ -491,7 +529,7 @@ struct FrontShared {
 
 // Factor one front (lower triangle in st), fully-summed columns 0..p-1.
 // Writes L (packed trapezoid), pivot kinds, permuted row ids, CB, inertia counters.
-template <int NT, int MR, class S>
+template <int NT, int MR, bool DF, class S>
 __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
                              double* coefA, double* coefB, const FactorArgs& A, int f, FrontShared* sh) {
     const int tid = threadIdx.x;
@@ -861,7 +899,11 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
 #pragma unroll
                 for (int b = 0; b <= a; ++b) {
                     const int j = tx + G * b;
-                    if (i < m && j >= p && j <= i) cb[((i - p) * (i - p + 1)) / 2 + (j - p)] = R[a][b];
+                    if (i < m && j >= p && j <= i) {
+                        double* dst = cb + ((i - p) * (i - p + 1)) / 2 + (j - p);
+                        if (DF) st_sc1(dst, R[a][b]);
+                        else *dst = R[a][b];
+                    }
                 }
             }
         }
@@ -880,7 +922,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             }
 #pragma unroll
             for (int u = 0; u < WB; ++u)
-                if (t0 + u * NT < ctot) cb[t0 + u * NT] = v[u];
+                if (t0 + u * NT < ctot) {
+                    if (DF) st_sc1(cb + t0 + u * NT, v[u]);
+                    else cb[t0 + u * NT] = v[u];
+                }
         }
     }
     if (sub) A.stamps[8 * f + 7] = __builtin_amdgcn_s_memrealtime();
@@ -898,7 +943,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
 // Latency-bound (a few KB per front), so the loads are grouped into as few dependent round trips as
 // possible: {rows, first entry batch, children's edge metadata} -> {scales} -> {per child: CB values
 // and both relmap entries of each element together}.
-template <int NT, class S>
+template <int NT, bool DF, class S>
 __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
                                const FactorArgs& A, int f) {
     const int tid = threadIdx.x, lane = tid & 63;
@@ -949,6 +994,8 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
         }
     }
     if (asm_st) { __builtin_amdgcn_s_waitcnt(0); A.stamps[8 * f + 5] = __builtin_amdgcn_s_memrealtime(); }
+    // dataflow schedule: children factored in this launch have published their contribution blocks
+    if (DF && A.df_nch[f] > 0) df_wait(A.df_cnt + f, A.df_epoch * (uint32_t)A.df_nch[f], A.df_abort);
     // children: contribution blocks are row-major packed lower triangles (row r: columns 0..r);
     // relmap maps child CB rows to ascending parent rows, so (rm[r], rm[c]) is in the lower triangle.
     // Children are taken in pairs whose first batches are loaded together (the loads of a child are
@@ -966,7 +1013,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
             const int t = t0 + u * NT;
             int r = 0, c = 0;
             if (t < ctot) tri_rc(t, r, c);
-            b.v[u] = t < ctot ? cb[t] : 0.0;
+            b.v[u] = t < ctot ? (DF ? ld_sc1(cb + t) : cb[t]) : 0.0;
             gi[u] = rm[r];
             gj[u] = rm[c];
         }
@@ -1037,10 +1084,43 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 
     int32_t* rstage = lrow + m;
     int8_t* pk = (int8_t*)(rstage + m);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
-    assemble_front<NT>(st, fsize, m, p, lrow, sloc, rstage, A, f);
+    assemble_front<NT, false>(st, fsize, m, p, lrow, sloc, rstage, A, f);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front<NT, MR>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    factor_front<NT, MR, false>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
+}
+
+// Dataflow factorization of the upper part of the assembly tree (every front one-wave, m <= 64):
+// ONE launch, a resident grid of one-wave blocks walks A.df_order (children before parents; block b
+// takes positions b, b + grid, ...).  A front assembles its original entries, waits for its children
+// of this launch (arrival counter, sc1 poll), reads their contribution blocks with sc1 loads, factors,
+// writes its own contribution block with sc1 stores and, after the wave's vmcnt(0), adds one to its
+// parent's counter.  Children factored by the earlier level launches are complete before the launch.
+template <int MR>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_df(FactorArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
+    for (int t = blockIdx.x; t < A.df_nf; t += gridDim.x) {
+        const int f = A.df_order[t];
+        const int m = A.fm[f], p = A.fp[f];
+        const PackedStore st{smem + 4};
+        const int64_t fsize = packed_even(m);
+        double* sloc = smem + 4 + fsize;
+        double* coefB = sloc + m;
+        int32_t* lrow = (int32_t*)(coefB + m);
+        int32_t* rstage = lrow + m;
+        int8_t* pk = (int8_t*)(rstage + m);
+        if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
+        assemble_front<64, true>(st, fsize, m, p, lrow, sloc, rstage, A, f);
+        if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
+        factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+        if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
+        const int par = A.fparent[f];
+        drain_stores();
+        if (par >= 0 && threadIdx.x == 0)
+            __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __syncthreads();  // LDS reused by the next front
+    }
 }
 
 __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const int32_t* __restrict__ fronts) {
@@ -1054,8 +1134,8 @@ __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const 
     int32_t* lrow = (int32_t*)(coefB + m);
     int32_t* rstage = lrow + m;
     int8_t* pk = (int8_t*)(rstage + m);
-    assemble_front<kThreads>(st, (int64_t)m * m, m, p, lrow, sloc, rstage, A, f);
-    factor_front<kThreads, 0>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    assemble_front<kThreads, false>(st, (int64_t)m * m, m, p, lrow, sloc, rstage, A, f);
+    factor_front<kThreads, 0, false>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -1285,38 +1365,7 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, int64_
     }
 }
 
-__device__ __forceinline__ double ld_sc1(const double* p) {
-    return as_double(__hip_atomic_load((const unsigned long long*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void st_sc1(double* p, double v) {
-    __hip_atomic_store((unsigned long long*)p, as_bits(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 
-constexpr int kDfSpinLimit = 1 << 22;  // polls (each behind s_sleep 2): about a second
-
-// Poll *addr (sc1) until it reaches `target` (wrap-safe); false on abort / limit.  Wave-uniform.
-__device__ __noinline__ bool df_wait(const uint32_t* addr, uint32_t target, uint32_t* abort_flag) {
-    uint32_t v = ld_sc1_u32(addr);
-    int it = 0;
-    while ((int32_t)(v - target) < 0) {
-        __builtin_amdgcn_s_sleep(2);
-        v = ld_sc1_u32(addr);
-        if ((++it & 63) == 0) {
-            if (ld_sc1_u32(abort_flag)) return false;
-            if (it >= kDfSpinLimit) {
-                __hip_atomic_store(abort_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                return false;
-            }
-        }
-    }
-    return true;
-}
-
-// every store of this wave has completed (sc1 stores: written through) before the signal below
-__device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 // ---- per-front pieces shared by both schedules ----
 
@@ -1907,6 +1956,23 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
     const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;
     if (forward) hipLaunchKernelGGL(k_solve_fwd_w, dim3(count), dim3(64), sh, s, A, fronts);
     else hipLaunchKernelGGL(k_solve_bwd_w, dim3(count), dim3(64), sh, s, A, fronts);
+    return hipGetLastError();
+}
+
+int factor_df_grid(int mmax, int nf) {
+    const size_t sh = factor_lds_bytes(mmax);
+    int dev = 0, cus = 0, nb = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_factor_df<8>, 64, sh) != hipSuccess) return 0;
+    const int per_cu = nb - 1;  // one below the reported residency (the query can over-report by one)
+    if (per_cu < 1) return 0;
+    return (int)std::min<int64_t>((int64_t)per_cu * cus, std::max(nf, 1));
+}
+
+hipError_t launch_factor_df(const FactorArgs& A, int grid, int mmax, hipStream_t s) {
+    if (A.df_nf <= 0 || grid <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_factor_df<8>, dim3(grid), dim3(64), factor_lds_bytes(mmax), s, A);
     return hipGetLastError();
 }
 

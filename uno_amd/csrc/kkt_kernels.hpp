@@ -45,6 +45,13 @@ struct FactorArgs {
     int stamp_mode;  // 1: phases + cycle counts, 2: write-out sub-phases in slots 4..7  // diagnostics (nullptr in normal runs): per front 8 words
     double u;
     double null_fac;
+    // dataflow schedule of the upper tree (k_factor_df), after the level launches of the lower levels
+    const int32_t* df_order;    // fronts, children before parents
+    int32_t df_nf;
+    const int32_t* df_nch;      // per front: children in the dataflow set
+    uint32_t* df_cnt;           // per front: children arrived (cumulative: epoch * df_nch when complete)
+    uint32_t df_epoch;
+    uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
 };
 
 struct SolveArgs {
@@ -149,6 +156,9 @@ hipError_t launch_unscale(const double* w, const double* scale, double* x, int64
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
                         hipStream_t s);
 
+// dataflow factorization of the upper tree (one-wave fronts, m <= 64)
+int factor_df_grid(int mmax, int nf);
+hipError_t launch_factor_df(const FactorArgs& A, int grid, int mmax, hipStream_t s);
 // dataflow solve: one resident grid of one-wave blocks per direction (grid from the occupancy query)
 int solve_df_grid(int lds_doubles, int nf);
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);

@@ -32,7 +32,7 @@ class KKTStats(ctypes.Structure):
         ("pivots_relaxed", ctypes.c_int64), ("factorizations", ctypes.c_int64), ("solves", ctypes.c_int64),
         ("flops", ctypes.c_double), ("analysis_seconds", ctypes.c_double), ("bytes_L", ctypes.c_double),
         ("bytes_cb", ctypes.c_double), ("fronts_merged", ctypes.c_int64), ("solve_grid", ctypes.c_int64),
-        ("solve_aborts", ctypes.c_int64),
+        ("solve_aborts", ctypes.c_int64), ("factor_df_fronts", ctypes.c_int64), ("factor_df_aborts", ctypes.c_int64),
     ]
 
     def as_dict(self):
