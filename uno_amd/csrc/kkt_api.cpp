@@ -152,11 +152,11 @@ struct uno_kkt {
     // "dataflow_factor" (default 1)
     int dff_enabled = 1;
     int dff_level = INT32_MAX;     // first level of the dataflow launch (INT32_MAX: none)
-    int dff_grid = 0, dff_mmax = 0;
+    int dff_mmax = 0;
     uint32_t dff_epoch = 0;
     int64_t dff_aborts = 0;
     DBuf<int32_t> dff_order, dff_nch;
-    DBuf<uint32_t> dff_cnt;
+    DBuf<uint32_t> dff_cnt, dff_ticket;
     // distributed factorization (null comm: one GPU)
     // device-side vector work around the solve
     int64_t rhs_n = -1, rhs_m = -1;
@@ -662,7 +662,6 @@ int finish_factorization(uno_kkt_t h) {
 hipError_t setup_factor_dataflow(uno_kkt_t h) {
     const Symbolic& S = h->S;
     h->dff_level = INT32_MAX;
-    h->dff_grid = 0;
     h->dff_epoch = 0;
     if (h->world > 1 || !h->dff_enabled || S.nf == 0) return hipSuccess;
     // lowest level from which every front fits the one-wave register kernel (m <= 64)
@@ -687,14 +686,14 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
     if ((e = h->dff_nch.upload(nch, s)) != hipSuccess) return e;
     if ((e = h->dff_cnt.alloc(S.nf)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(h->dff_cnt.p, 0, sizeof(uint32_t) * S.nf, s)) != hipSuccess) return e;
+    if (!h->dff_ticket.p && (e = h->dff_ticket.alloc(1)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(h->dff_ticket.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     if (!h->df_abort.p && (e = h->df_abort.alloc(1)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     h->dff_mmax = mmax;
-    h->dff_grid = factor_df_grid(mmax, (int)order.size());
-    if (h->dff_grid > 0) h->dff_level = L;
+    h->dff_level = L;
     if (h->verbose)
-        fprintf(stderr, "[uno_kkt] dataflow factorization: levels %d..%d, %zu fronts, grid %d\n", L, S.nlevels - 1,
-                order.size(), h->dff_grid);
+        fprintf(stderr, "[uno_kkt] dataflow factorization: levels %d..%d, %zu fronts\n", L, S.nlevels - 1, order.size());
     return hipSuccess;
 }
 
@@ -936,6 +935,7 @@ int enqueue_factorization(uno_kkt_t h) {
         A.stamps = h->stamps.p;
     }
     A.df_order = nullptr; A.df_nf = 0; A.df_nch = nullptr; A.df_cnt = nullptr; A.df_epoch = 0; A.df_abort = nullptr;
+    A.df_ticket = nullptr;
     const bool dff = h->world == 1 && h->dff_level != INT32_MAX;
     for (const Launch& L : h->plan[0].fac) {
         if (dff && L.level >= h->dff_level) continue;
@@ -950,7 +950,8 @@ int enqueue_factorization(uno_kkt_t h) {
         A.df_cnt = h->dff_cnt.p;
         A.df_epoch = ++h->dff_epoch;
         A.df_abort = h->df_abort.p;
-        HIPCHK(h, launch_factor_df(A, h->dff_grid, h->dff_mmax, s));
+        A.df_ticket = h->dff_ticket.p;
+        HIPCHK(h, launch_factor_df(A, h->dff_mmax, s));
         HIPCHK(h, hipMemcpyAsync(h->h_counters + 11, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
     if (h->world > 1) {

@@ -224,7 +224,7 @@ __device__ __forceinline__ uint32_t ld_sc1_u32(const uint32_t* p) {
 constexpr int kDfSpinLimit = 1 << 22;  // polls (each behind s_sleep 2): about a second
 
 // Poll *addr (sc1) until it reaches `target` (wrap-safe); false on abort / limit.  Wave-uniform.
-__device__ __noinline__ bool df_wait(const uint32_t* addr, uint32_t target, uint32_t* abort_flag) {
+__device__ __forceinline__ bool df_wait(const uint32_t* addr, uint32_t target, uint32_t* abort_flag) {
     uint32_t v = ld_sc1_u32(addr);
     int it = 0;
     while ((int32_t)(v - target) < 0) {
@@ -583,13 +583,24 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     const bool owner = tx == kk;
                     const double akk = readlane_d(R[bk][bk], kk * G + kk);
                     const double aak = fabs(akk);
-                    bool bad = false;
+                    // branch-free: every lane stores (non-owners into the trash slot F[-1]) and
+                    // reduces its candidates' |a_ik| with a max tree; u * max > |a_kk| is exactly
+                    // "some u |a_ik| > |a_kk|" (rounding of u * x is monotonic in x)
+                    double mx[RM];
 #pragma unroll
-                    for (int a = bk; a < RM; ++a) {
+                    for (int a = 0; a < RM; ++a) {
+                        mx[a] = 0.0;
+                        if (a < bk) continue;
                         const int i = ty + G * a;
-                        if (owner && i < m) colv[i] = R[a][bk];  // colv has m entries
-                        bad |= owner && (a > bk || i > k) && i < m && A.u * fabs(R[a][bk]) > aak;
+                        double* dst = (owner && i < m) ? colv + i : st.F - 1;  // colv has m entries
+                        *dst = R[a][bk];
+                        mx[a] = ((a > bk || i > k) && i < m) ? fabs(R[a][bk]) : 0.0;
                     }
+#pragma unroll
+                    for (int w = 1; w < RM; w *= 2)
+#pragma unroll
+                        for (int a = 0; a + w < RM; a += 2 * w) mx[a] = fmax(mx[a], mx[a + w]);
+                    const bool bad = owner && A.u * mx[0] > aak;
                     need = (__ballot(bad) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange
@@ -1001,7 +1012,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
     // Children are taken in pairs whose first batches are loaded together (the loads of a child are
     // one global round trip, mostly TLB / HBM latency at the upper levels); the additions are applied
     // child by child in a fixed order (deterministic sums).
-    constexpr int CB = NT == 64 ? 16 : 8;  // entries per lane per batch (one batch covers a 45-row CB at one wave)
+    constexpr int CB = 8;  // entries per lane per batch (8: the one-wave kernels stay within 168 VGPRs, 3 waves per SIMD)
     struct Batch {
         double v[CB];
         int pos[CB];
@@ -1071,7 +1082,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 __device__ __forceinline__ int64_t packed_even(int m) { return (((int64_t)m * (m + 1) / 2) + 1) & ~1ll; }
 
 template <int NT, int MR>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 3 : 1))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
     const int f = fronts[blockIdx.x];
@@ -1091,36 +1102,39 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(NT == 256 ? 
 }
 
 // Dataflow factorization of the upper part of the assembly tree (every front one-wave, m <= 64):
-// ONE launch, a resident grid of one-wave blocks walks A.df_order (children before parents; block b
-// takes positions b, b + grid, ...).  A front assembles its original entries, waits for its children
-// of this launch (arrival counter, sc1 poll), reads their contribution blocks with sc1 loads, factors,
-// writes its own contribution block with sc1 stores and, after the wave's vmcnt(0), adds one to its
-// parent's counter.  Children factored by the earlier level launches are complete before the launch.
+// ONE launch of one block per front.  A block draws a ticket (atomic counter) when it starts and takes
+// front A.df_order[ticket] (children before parents), so it only ever waits for fronts taken by blocks
+// that started before it: no residency assumption, no deadlock whatever the dispatch order.  A front
+// assembles its original entries, waits for its children of this launch (arrival counter, sc1 poll),
+// reads their contribution blocks with sc1 loads, factors, writes its own contribution block with sc1
+// stores and, after the wave's vmcnt(0), adds one to its parent's counter.  Children factored by the
+// earlier level launches are complete before the launch.
 template <int MR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_df(FactorArgs A) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_factor_df(FactorArgs A) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
-    for (int t = blockIdx.x; t < A.df_nf; t += gridDim.x) {
-        const int f = A.df_order[t];
-        const int m = A.fm[f], p = A.fp[f];
-        const PackedStore st{smem + 4};
-        const int64_t fsize = packed_even(m);
-        double* sloc = smem + 4 + fsize;
-        double* coefB = sloc + m;
-        int32_t* lrow = (int32_t*)(coefB + m);
-        int32_t* rstage = lrow + m;
-        int8_t* pk = (int8_t*)(rstage + m);
-        if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
-        assemble_front<64, true>(st, fsize, m, p, lrow, sloc, rstage, A, f);
-        if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-        factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
-        if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
-        const int par = A.fparent[f];
-        drain_stores();
-        if (par >= 0 && threadIdx.x == 0)
-            __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __syncthreads();  // LDS reused by the next front
-    }
+    uint32_t tk = 0;
+    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(A.df_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);  // lane 0 is the first active lane
+    const int t = (int)(tk - (A.df_epoch - 1u) * (uint32_t)A.df_nf);  // tickets are cumulative over launches
+    if (t < 0 || t >= A.df_nf) return;  // cannot happen with one block per front
+    const int f = A.df_order[t];
+    const int m = A.fm[f], p = A.fp[f];
+    const PackedStore st{smem + 4};
+    const int64_t fsize = packed_even(m);
+    double* sloc = smem + 4 + fsize;
+    double* coefB = sloc + m;
+    int32_t* lrow = (int32_t*)(coefB + m);
+    int32_t* rstage = lrow + m;
+    int8_t* pk = (int8_t*)(rstage + m);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
+    assemble_front<64, true>(st, fsize, m, p, lrow, sloc, rstage, A, f);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
+    factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
+    const int par = A.fparent[f];
+    drain_stores();
+    if (par >= 0 && threadIdx.x == 0) __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const int32_t* __restrict__ fronts) {
@@ -1959,20 +1973,9 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
     return hipGetLastError();
 }
 
-int factor_df_grid(int mmax, int nf) {
-    const size_t sh = factor_lds_bytes(mmax);
-    int dev = 0, cus = 0, nb = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return 0;
-    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, k_factor_df<8>, 64, sh) != hipSuccess) return 0;
-    const int per_cu = nb - 1;  // one below the reported residency (the query can over-report by one)
-    if (per_cu < 1) return 0;
-    return (int)std::min<int64_t>((int64_t)per_cu * cus, std::max(nf, 1));
-}
-
-hipError_t launch_factor_df(const FactorArgs& A, int grid, int mmax, hipStream_t s) {
-    if (A.df_nf <= 0 || grid <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_factor_df<8>, dim3(grid), dim3(64), factor_lds_bytes(mmax), s, A);
+hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
+    if (A.df_nf <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax), s, A);
     return hipGetLastError();
 }
 

@@ -50,7 +50,8 @@ struct FactorArgs {
     int32_t df_nf;
     const int32_t* df_nch;      // per front: children in the dataflow set
     uint32_t* df_cnt;           // per front: children arrived (cumulative: epoch * df_nch when complete)
-    uint32_t df_epoch;
+    uint32_t df_epoch;          // 1, 2, ... per factorization since the counters were cleared
+    uint32_t* df_ticket;        // block start order (cumulative: (epoch - 1) * df_nf at launch)
     uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
 };
 
@@ -157,8 +158,7 @@ hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, in
                         hipStream_t s);
 
 // dataflow factorization of the upper tree (one-wave fronts, m <= 64)
-int factor_df_grid(int mmax, int nf);
-hipError_t launch_factor_df(const FactorArgs& A, int grid, int mmax, hipStream_t s);
+hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
 // dataflow solve: one resident grid of one-wave blocks per direction (grid from the occupancy query)
 int solve_df_grid(int lds_doubles, int nf);
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
