@@ -326,14 +326,16 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
         // front).  Finer LDS classes ({16, 24, .., 128}) were measured slower on C3 (2.36 vs 1.99 ms):
         // the one-wave kernel is VALU-issue bound at levels 0-1 and more co-resident fronts per CU
         // only lengthen every front; a class smaller than kMinClass absorbs the next smaller one.
-        static const int caps[] = {32, 64, 128};
+        static const int caps[] = {32, 64, kMaxWaveFront, 128};
         constexpr int kMinClass = 2048;
         auto prev_cap = [](int c) {
             int pc = 0;
             for (int x : caps) if (x < c) pc = x;
             return pc;
         };
-        auto kernel_of = [](int mm) { return mm > kMaxLdsFront ? 3 : (mm > 64 ? 2 : (mm > 32 ? 1 : 0)); };
+        auto kernel_of = [](int mm) {
+            return mm > kMaxLdsFront ? 4 : (mm > kMaxWaveFront ? 3 : (mm > 64 ? 2 : (mm > 32 ? 1 : 0)));
+        };
         const int e = (int)lv.size();
         int q = 0;
         while (q < e) {

@@ -1082,7 +1082,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 __device__ __forceinline__ int64_t packed_even(int m) { return (((int64_t)m * (m + 1) / 2) + 1) & ~1ll; }
 
 template <int NT, int MR>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(3))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MR > 8 ? 2 : 3))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
     const int f = fronts[blockIdx.x];
@@ -1874,7 +1874,7 @@ hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hip
 size_t factor_lds_bytes(int mmax) {
     const size_t packed = (((size_t)mmax * (mmax + 1) / 2) + 1) & ~(size_t)1;
     // + slack: the register path reads the column vector (coefB) unclamped up to 2*kThreads... entries
-    const int grid_rows = mmax <= 32 ? 32 : (mmax <= 64 ? 64 : 2 * kThreads);
+    const int grid_rows = mmax <= 32 ? 32 : (mmax <= 64 ? 64 : (mmax <= kMaxWaveFront ? kMaxWaveFront : 2 * kThreads));
     return 32 + packed * sizeof(double) + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
            (size_t)((mmax + 15) & ~15) + (size_t)grid_rows * sizeof(double);
 }
@@ -1890,6 +1890,7 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
         // larger fronts: four waves on a 16x16 update grid
         if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= 64) hipLaunchKernelGGL((k_factor_lds<64, 8>), dim3(count), dim3(64), sh, s, A, fronts);
+        else if (mmax <= kMaxWaveFront) hipLaunchKernelGGL((k_factor_lds<64, 9>), dim3(count), dim3(64), sh, s, A, fronts);
         else hipLaunchKernelGGL((k_factor_lds<kThreads, 8>), dim3(count), dim3(kThreads), sh, s, A, fronts);
     }
     return hipGetLastError();

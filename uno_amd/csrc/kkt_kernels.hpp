@@ -168,7 +168,8 @@ hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32
 hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s);
 hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, double* x, int64_t n, hipStream_t s);
 
-constexpr int kMaxLdsFront = 128;     // fronts up to this order factor entirely in LDS
+constexpr int kMaxLdsFront = 128;
+constexpr int kMaxWaveFront = 72;     // one-wave register-resident factorization (8 x 8 lane grid, 9 row blocks)     // fronts up to this order factor entirely in LDS
 constexpr int kMaxGlobalFront = 8192; // larger fronts are rejected at analysis
 
 }  // namespace ukkt
