@@ -142,7 +142,7 @@ struct uno_kkt {
     bool df_rx_valid = false;      // rxpos matches the last factorization's pivoting
     bool df_check = false;         // a dataflow solve's abort flag copy is pending
     int64_t df_aborts = 0;
-    DBuf<int32_t> df_order, df_xpos, df_rxpos;
+    DBuf<int32_t> df_order, df_desc, df_xpos, df_rxpos;
     DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
     DBuf<uint32_t> df_cnt, df_done, df_abort;
     DBuf<double> df_cvx, df_xs;
@@ -245,7 +245,7 @@ int enqueue_factorization(uno_kkt_t h);
 
 DfArgs dataflow_args(uno_kkt_t h) {
     DfArgs D;
-    D.order = h->df_order.p; D.nf = (int32_t)h->S.nf; D.parent = h->fparent.p; D.cnt = h->df_cnt.p;
+    D.order = h->df_order.p; D.desc = h->df_desc.p; D.nf = (int32_t)h->S.nf; D.parent = h->fparent.p; D.cnt = h->df_cnt.p;
     D.done = h->df_done.p; D.epoch = h->df_epoch; D.cvx = h->df_cvx.p; D.cvx_off = h->df_cvx_off.p;
     D.ch_cvx_off = h->df_ch_cvx_off.p; D.xs = h->df_xs.p; D.xs_off = h->df_xs_off.p; D.rxpos = h->df_rxpos.p;
     D.abort_flag = h->df_abort.p;
@@ -729,6 +729,19 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     hipStream_t s = h->stream;
     hipError_t e;
     if ((e = h->df_order.upload(S.level_fronts, s)) != hipSuccess) return e;
+    {
+        std::vector<int32_t> desc((size_t)S.nf * 16, 0);
+        auto put64 = [&](int32_t* d, int64_t v) { d[0] = (int32_t)(uint32_t)v; d[1] = (int32_t)(uint32_t)((uint64_t)v >> 32); };
+        for (int64_t t = 0; t < S.nf; ++t) {
+            const int32_t f = S.level_fronts[t];
+            int32_t* d = desc.data() + 16 * t;
+            d[kDescF] = f; d[kDescM] = S.f_m[f]; d[kDescP] = S.f_p[f]; d[kDescPar] = S.f_parent[f];
+            d[kDescC0] = S.f_child_off[f]; d[kDescC1] = S.f_child_off[f + 1];
+            put64(d + kDescRo, S.f_rows_off[f]); put64(d + kDescLo, S.f_L_off[f]);
+            put64(d + kDescCvx, cvx[f]); put64(d + kDescXs, xs[f]);
+        }
+        if ((e = h->df_desc.upload(desc, s)) != hipSuccess) return e;
+    }
     if ((e = h->df_cvx_off.upload(cvx, s)) != hipSuccess) return e;
     if ((e = h->df_ch_cvx_off.upload(chx, s)) != hipSuccess) return e;
     if ((e = h->df_xs_off.upload(xs, s)) != hipSuccess) return e;

@@ -1590,19 +1590,24 @@ struct FrontPre {
     double2 v[kPre];
 };
 
-template <bool FWD>
-__device__ __forceinline__ FrontRec df_record(const SolveArgs& A, const DfArgs& D, int f) {
+// A front's record lives in DfArgs::desc (16 words per walk position, kDesc* fields): one dword per
+// lane, loaded a whole phase before the fields are extracted with readlane, so the load is never
+// waited for alone (a uniform load consumed at once would stall the wave for a full round trip).
+__device__ __forceinline__ int df_desc_load(const DfArgs& D, int pos) { return D.desc[pos * 16 + (threadIdx.x & 15)]; }
+__device__ __forceinline__ FrontRec df_record(int dv) {
+    auto w = [&](int k) { return __builtin_amdgcn_readlane(dv, k); };
+    auto w64 = [&](int k) { return (int64_t)(((uint64_t)(uint32_t)w(k + 1) << 32) | (uint32_t)w(k)); };
     FrontRec r;
-    r.f = f;
-    r.m = A.fm[f];
-    r.p = A.fp[f];
-    r.ro = A.rows_off[f];
-    r.Lo = A.L_off[f];
-    r.par = D.parent[f];
-    r.c0 = FWD ? A.child_off[f] : 0;
-    r.c1 = FWD ? A.child_off[f + 1] : 0;
-    r.xoff = FWD ? D.cvx_off[f] : 0;
-    r.woff = D.xs_off[f];
+    r.f = w(kDescF);
+    r.m = w(kDescM);
+    r.p = w(kDescP);
+    r.par = w(kDescPar);
+    r.c0 = w(kDescC0);
+    r.c1 = w(kDescC1);
+    r.ro = w64(kDescRo);
+    r.Lo = w64(kDescLo);
+    r.xoff = w64(kDescCvx);
+    r.woff = w64(kDescXs);
     r.sz = r.p * r.m - r.p * (r.p - 1) / 2;
     return r;
 }
@@ -1677,12 +1682,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     int t = blockIdx.x;
     if (t >= D.nf) return;
     FrontPre q;
-    q.r = df_record<true>(A, D, D.order[t]);
+    q.r = df_record(df_desc_load(D, t));
     df_issue<true>(A, D, q);
+    // The previous front's signal is deferred past this front's first dependent loads, so its store
+    // drain overlaps them; it is sent before any wait (this front may be that front's parent).
+    int pend = -1;
+    auto signal = [&]() {
+        drain_stores();
+        if (pend >= 0 && lane == 0) __hip_atomic_fetch_add(D.cnt + pend, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend = -1;
+    };
     for (; t < D.nf; t += gridDim.x) {
         // next position (clamped: the last front re-prefetches itself, branch-free loop-carried loads)
         const int tn = min(t + (int)gridDim.x, D.nf - 1);
-        const FrontRec rn = df_record<true>(A, D, D.order[tn]);  // used after the children's loads
+        const int dn = df_desc_load(D, tn);  // next record: extracted after the children's loads
         const int m = q.r.m, p = q.r.p, f = q.r.f, par = q.r.par, mypiv = q.mypiv;
         const int64_t xoff = q.r.xoff, woff = q.r.woff;
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f : nullptr;
@@ -1693,21 +1706,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         if (lane < m) { y[lane] = q.e0; fpl[lane] = q.fp0; }
         if (lane + 64 < m) { y[lane + 64] = 0.0; fpl[lane + 64] = q.fp1; }
         const uint32_t target = D.epoch * (uint32_t)(q.r.c1 - q.r.c0);
-        if ((int32_t)(q.dep - target) < 0) df_wait(D.cnt + f, target, D.abort_flag);
+        if ((int32_t)(q.dep - target) < 0) {
+            signal();
+            df_wait(D.cnt + f, target, D.abort_flag);
+        }
         df_stage(A, q, P);
         __syncthreads();
         fwd_extend_add<true>(A, D, q.r.c0, q.r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
         __syncthreads();
+        signal();
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-        q.r = rn;
+        q.r = df_record(dn);
         df_issue<true>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         fwd_compute<true>(m, p, P, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
-        drain_stores();
-        if (par >= 0 && lane == 0) __hip_atomic_fetch_add(D.cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend = par;
         __syncthreads();  // LDS reused by the next front
     }
+    signal();
 }
 
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_solve_bwd_df(SolveArgs A, DfArgs D) {
@@ -1716,11 +1733,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     int t = blockIdx.x;
     if (t >= D.nf) return;
     FrontPre q;
-    q.r = df_record<false>(A, D, D.order[D.nf - 1 - t]);
+    q.r = df_record(df_desc_load(D, D.nf - 1 - t));
     df_issue<false>(A, D, q);
+    int pend = -1;  // deferred publication of the previous front (see k_solve_fwd_df)
+    auto signal = [&]() {
+        drain_stores();
+        if (pend >= 0 && lane == 0) __hip_atomic_store(D.done + pend, D.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend = -1;
+    };
     for (; t < D.nf; t += gridDim.x) {
         const int tn = min(t + (int)gridDim.x, D.nf - 1);
-        const FrontRec rn = df_record<false>(A, D, D.order[D.nf - 1 - tn]);
+        const int dn = df_desc_load(D, D.nf - 1 - tn);
         const int m = q.r.m, p = q.r.p, f = q.r.f, mypiv = q.mypiv;
         const int64_t woff = q.r.woff;
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f + 4 : nullptr;
@@ -1729,22 +1752,26 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         double* x = smem_s + ((q.r.sz + 1) & ~1);
         // own pivots: z of the forward solve; contribution rows: the ancestors' published solution
         // values (this launch), through the per-row slot index rxpos, once the parent has published
-        if (q.r.par >= 0 && (int32_t)(q.dep - D.epoch) < 0) df_wait(D.done + q.r.par, D.epoch, D.abort_flag);
+        if (q.r.par >= 0 && (int32_t)(q.dep - D.epoch) < 0) {
+            signal();
+            df_wait(D.done + q.r.par, D.epoch, D.abort_flag);
+        }
         if (lane < m) x[lane] = lane < p ? q.e0 : ld_sc1(D.xs + q.a0);
         if (lane + 64 < m) x[lane + 64] = ld_sc1(D.xs + q.a1);
         df_stage(A, q, P);
         __syncthreads();
+        signal();
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-        q.r = rn;
+        q.r = df_record(dn);
         df_issue<false>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         const double xj = bwd_compute(m, p, P, x, mypiv);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (lane < p) st_sc1(D.xs + woff + lane, xj);
-        drain_stores();
-        if (lane == 0) __hip_atomic_store(D.done + f, D.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        pend = f;
         __syncthreads();
     }
+    signal();
 }
 
 // right-hand side into elimination order (xs[xpos[i]] = s_i b_i) and the solution back (x_i = s_i xs[xpos[i]])

@@ -75,8 +75,11 @@ struct SolveArgs {
 };
 
 // Dataflow (one launch per direction) solve schedule, kkt_kernels.hip k_solve_fwd_df / k_solve_bwd_df
+// walk-order front records of the dataflow solve: 16 int32 per position
+enum : int { kDescF = 0, kDescM, kDescP, kDescPar, kDescC0, kDescC1, kDescRo = 6, kDescLo = 8, kDescCvx = 10, kDescXs = 12 };
 struct DfArgs {
     const int32_t* order;       // fronts, children before parents (the backward solve walks it from the end)
+    const int32_t* desc;        // per walk position: 16-word record (kDesc* fields, 64-bit fields low word first)
     int32_t nf;
     const int32_t* parent;      // assembly-tree parent (-1 = root)
     uint32_t* cnt;              // forward: children arrived; epoch * children once all have (cumulative)
