@@ -13,4 +13,5 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/$R/pmc
 python tools/rocpd_summary.py stats gpurun_out/$R/trace/run_results.db gpurun_out/$R/kernel_stats.csv
 python tools/rocpd_summary.py pmc gpurun_out/$R/pmc_fetch/run_results.db gpurun_out/$R/pmc_fetch.json > /dev/null
 python tools/rocpd_summary.py pmc gpurun_out/$R/pmc_write/run_results.db gpurun_out/$R/pmc_write.json > /dev/null
+python tools/pmc_traffic.py gpurun_out/$R/pmc_fetch.json gpurun_out/$R/pmc_write.json gpurun_out/$R/pmc_traffic.json > /dev/null
 echo done

@@ -14,7 +14,7 @@ import sqlite3
 import sys
 
 GROUPS = {
-    "factor": ("k_factor_lds", "k_factor_global"),
+    "factor": ("k_factor_lds", "k_factor_global", "k_factor_df"),
     "solve": ("k_solve_fwd", "k_solve_bwd"),
     "pack": ("k_pack",),
     "scale": ("k_rowscan", "k_normmax", "k_scale_update"),
@@ -44,9 +44,9 @@ def stats(db, out):
 
 def pmc(db, out):
     c = sqlite3.connect(db)
-    # factorizations = k_pack dispatches, solves = k_unscale dispatches (one each per call)
+    # factorizations = k_pack dispatches, solves = k_unscale / k_xs_out dispatches (one per call)
     nfac = c.execute("select count(distinct dispatch_id) from counters_collection where kernel_name like '%k_pack%'").fetchone()[0]
-    nsol = c.execute("select count(distinct dispatch_id) from counters_collection where kernel_name like '%k_unscale%'").fetchone()[0]
+    nsol = c.execute("select count(distinct dispatch_id) from counters_collection where kernel_name like '%k_unscale%' or kernel_name like '%k_xs_out%'").fetchone()[0]
     rows = c.execute("select kernel_name, counter_name, sum(value), count(*), sum(duration) "
                      "from counters_collection group by kernel_name, counter_name").fetchall()
     res = {"factorizations": nfac, "solves": nsol, "per_run": {}, "note": "KB per factorization (solve group: per solve); "
