@@ -113,6 +113,8 @@ def test_distributed_arrowband(ua, world):
     info0 = out[0][1]
     assert info0["world"] == world and info0["subtrees"] >= world
     assert sum(o[1]["my_fronts"] for o in out) + info0["top_fronts"] == single.stats()["n_fronts"]
+    # the ranks' own subtrees use the dataflow factorization of their upper levels too
+    assert sum(o[2]["factor_df_fronts"] for o in out) > 0 and all(o[2]["factor_df_aborts"] == 0 for o in out)
     for k, vv in enumerate((v, v2)):
         for q in range(world):
             assert out[q][0][k][0] == ref[k][0], (q, k)      # inertia all-reduced to every rank

@@ -665,22 +665,30 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
     const Symbolic& S = h->S;
     h->dff_level = INT32_MAX;
     h->dff_epoch = 0;
-    if (h->world > 1 || !h->dff_enabled || S.nf == 0) return hipSuccess;
-    // lowest level from which every front fits the one-wave register kernel (m <= 64)
+    if (!h->dff_enabled || S.nf == 0) return hipSuccess;
+    // the fronts of plan[0]: all fronts on one GPU, the rank's own subtrees in a distributed run (the
+    // top fronts are factored after the root exchange by the level launches of plan[1])
+    auto mine = [&](int32_t f) { return h->world == 1 || h->dist.part.owner[f] == h->rank; };
+    // lowest level from which every own front fits the one-wave register kernel (m <= 64)
     int L = S.nlevels;
     while (L > 0) {
         bool ok = true;
-        for (int q = S.level_off[L - 1]; q < S.level_off[L] && ok; ++q) ok = S.f_m[S.level_fronts[q]] <= 64;
+        for (int q = S.level_off[L - 1]; q < S.level_off[L] && ok; ++q)
+            ok = !mine(S.level_fronts[q]) || S.f_m[S.level_fronts[q]] <= 64;
         if (!ok) break;
         --L;
     }
     if (L >= S.nlevels) return hipSuccess;
-    std::vector<int32_t> order(S.level_fronts.begin() + S.level_off[L], S.level_fronts.begin() + S.level_off[S.nlevels]);
+    std::vector<int32_t> order;
+    for (int q = S.level_off[L]; q < S.level_off[S.nlevels]; ++q)
+        if (mine(S.level_fronts[q])) order.push_back(S.level_fronts[q]);
+    if (order.empty()) return hipSuccess;
     std::vector<int32_t> nch(S.nf, 0);
     int mmax = 1;
     for (int32_t f : order) {
         mmax = std::max(mmax, S.f_m[f]);
-        for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1]; ++q) nch[f] += S.f_level[S.child[q]] >= L;
+        for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1]; ++q)
+            nch[f] += S.f_level[S.child[q]] >= L && mine(S.child[q]);
     }
     hipStream_t s = h->stream;
     hipError_t e;
@@ -704,7 +712,6 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     h->df_grid = 0;
     h->df_rx_valid = false;
     h->df_epoch = 0;
-    if (hipError_t e = setup_factor_dataflow(h); e != hipSuccess) return e;
     if (h->world > 1 || !h->df_enabled || S.nf == 0) return hipSuccess;
     int lds = 0;
     for (int64_t f = 0; f < S.nf; ++f) {
@@ -869,6 +876,7 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, build_plan(h, [](int32_t) { return true; }, h->plan[0]));
         HIPCHK(h, build_plan(h, [](int32_t) { return false; }, h->plan[1]));
     }
+    HIPCHK(h, setup_factor_dataflow(h));  // after the partition: a rank's own subtrees
     HIPCHK(h, hipStreamSynchronize(s));
     double an = h->st.analysis_seconds;
     int64_t nfac = h->st.factorizations, nsol = h->st.solves;
@@ -951,7 +959,7 @@ int enqueue_factorization(uno_kkt_t h) {
     }
     A.df_order = nullptr; A.df_nf = 0; A.df_nch = nullptr; A.df_cnt = nullptr; A.df_epoch = 0; A.df_abort = nullptr;
     A.df_ticket = nullptr;
-    const bool dff = h->world == 1 && h->dff_level != INT32_MAX;
+    const bool dff = h->dff_level != INT32_MAX;
     for (const Launch& L : h->plan[0].fac) {
         if (dff && L.level >= h->dff_level) continue;
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
