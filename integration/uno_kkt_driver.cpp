@@ -4,7 +4,7 @@
 // factorization the plugin performed.  This is the in-container stand-in for `uno_ampl model.nl -AMPL
 // preset=ipopt linear_solver=HIPLDL` (bindings/AMPL/uno_ampl.cpp:78-139; ASL is not available).
 //
-// usage: uno_kkt_driver <model> [option=value ...]     model: hs015
+// usage: uno_kkt_driver <model> [option=value ...]     model: hs015 (hand-coded) or a path to a text .nl file
 #include <cstdio>
 #include <iostream>
 #include <memory>
@@ -14,6 +14,7 @@
 #include "Uno.hpp"
 #include "model/ModelFactory.hpp"
 #include "models/HS015Model.hpp"
+#include "models/NLModel.hpp"
 #include "optimization/Iterate.hpp"
 #include "optimization/Result.hpp"
 #include "options/DefaultOptions.hpp"
@@ -43,6 +44,9 @@ int main(int argc, char* argv[]) {
       std::unique_ptr<Model> model;
       if (model_name == "hs015") {
          model = std::make_unique<HS015Model>();
+      }
+      else if (model_name.size() > 3 && model_name.compare(model_name.size() - 3, 3, ".nl") == 0) {
+         model = std::make_unique<NLModel>(model_name);  // ASL-free .nl reader (models/NLModel.hpp)
       }
       else {
          throw std::invalid_argument("unknown model " + model_name);

@@ -1,0 +1,10 @@
+#!/bin/bash
+# Golden traces of the reference Uno core (libuno built from /root/reference by oracle/ref/Makefile)
+# with the oracle plugin (linear_solver=ORACLE) on the reference's example .nl files, read by the
+# ASL-free reader integration/models/NLModel.hpp.  hs015.nl / polak5.nl are copies of
+# /root/reference/examples/*.nl (model data).  Run from the repository root after `make -C oracle/ref`.
+set -e
+for m in hs015 polak5; do
+  oracle/_ref/uno_kkt_driver tests/golden/$m.nl linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
+    | sed "s#\"model\": \"tests/golden/$m.nl\"#\"model\": \"$m.nl\"#" > tests/golden/${m}_nl_uno_oracle.json
+done
