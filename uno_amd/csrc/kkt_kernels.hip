@@ -583,6 +583,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     const bool owner = tx == kk;
                     const double akk = readlane_d(R[bk][bk], kk * G + kk);
                     const double aak = fabs(akk);
+                    const double dinv = 1.0 / akk;  // issued before the test: overlaps it
                     // branch-free: every lane stores (non-owners into the trash slot F[-1]) and
                     // reduces its candidates' |a_ik| with a max tree; u * max > |a_kk| is exactly
                     // "some u |a_ik| > |a_kk|" (rounding of u * x is monotonic in x)
@@ -605,7 +606,6 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange
                         minpiv = fmin(minpiv, aak);
-                        const double dinv = 1.0 / akk;
                         double lv[RM], cv[RM];
 #pragma unroll
                         for (int a = bk; a < RM; ++a) {
