@@ -5,7 +5,7 @@ import numpy as np
 import uno_amd
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1000000
 N, nv, m, r, c, v, b = uno_amd.arrowband(n, uno_amd.SEEDS["C3"])
-for dff in (1, 0):
+for dff in (2, 1, 0):
     g = uno_amd.HipKKT(0, verbose=1, dataflow_factor=dff)
     g.analyze(N, r, c)
     g.factorize(v); g.inertia()

@@ -134,6 +134,7 @@ struct uno_kkt {
     int64_t max_long = 0;
     unsigned long long* h_counters = nullptr;
     Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
+    Plan dff_plan; // factor launches of the own fronts outside the dataflow launch (dff active)
     // dataflow solve (one launch per direction, kkt_kernels.hip k_solve_*_df); single GPU, every front
     // one-wave eligible; option "dataflow_solve" (default 1)
     int df_enabled = 1;
@@ -150,7 +151,7 @@ struct uno_kkt {
     DBuf<unsigned long long> df_stamps;
     // dataflow factorization of the upper tree (levels >= dff_level, every front one-wave); option
     // "dataflow_factor" (default 1)
-    int dff_enabled = 1;
+    int dff_enabled = 1;  // 0 off, 1 (default) levels >= L*, 2 also the small fronts below them (measured no faster at C3)
     int dff_level = INT32_MAX;     // first level of the dataflow launch (INT32_MAX: none)
     int dff_mmax = 0;
     uint32_t dff_epoch = 0;
@@ -679,17 +680,35 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
         --L;
     }
     if (L >= S.nlevels) return hipSuccess;
-    std::vector<int32_t> order;
+    // the set grows downwards (option 2, default): every own front of order <= M (M = largest order at
+    // levels >= L, so the launch keeps that LDS size) whose ancestors are all <= M; the rest (downward
+    // closed: a front above M makes its whole subtree "low") runs in level launches before
+    int M = 1;
     for (int q = S.level_off[L]; q < S.level_off[S.nlevels]; ++q)
-        if (mine(S.level_fronts[q])) order.push_back(S.level_fronts[q]);
+        if (mine(S.level_fronts[q])) M = std::max(M, S.f_m[S.level_fronts[q]]);
+    std::vector<char> in(S.nf, 0);
+    for (int l = S.nlevels - 1; l >= 0; --l) {
+        for (int q = S.level_off[l]; q < S.level_off[l + 1]; ++q) {
+            const int32_t f = S.level_fronts[q];
+            if (!mine(f)) continue;
+            const int32_t par = S.f_parent[f];
+            const bool parent_ok = par < 0 || !mine(par) || in[par];
+            in[f] = l >= L || (h->dff_enabled >= 2 && parent_ok && S.f_m[f] <= M);
+        }
+    }
+    std::vector<int32_t> order;
+    for (int q = 0; q < S.level_off[S.nlevels]; ++q)
+        if (in[S.level_fronts[q]]) order.push_back(S.level_fronts[q]);
     if (order.empty()) return hipSuccess;
     std::vector<int32_t> nch(S.nf, 0);
     int mmax = 1;
     for (int32_t f : order) {
         mmax = std::max(mmax, S.f_m[f]);
-        for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1]; ++q)
-            nch[f] += S.f_level[S.child[q]] >= L && mine(S.child[q]);
+        for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1]; ++q) nch[f] += in[S.child[q]];
     }
+    // level launches of the other own fronts (downward closed: all their descendants are among them)
+    if (hipError_t e = build_plan(h, [&](int32_t f) { return mine(f) && !in[f]; }, h->dff_plan); e != hipSuccess)
+        return e;
     hipStream_t s = h->stream;
     hipError_t e;
     if ((e = h->dff_order.upload(order, s)) != hipSuccess) return e;
@@ -703,7 +722,8 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
     h->dff_mmax = mmax;
     h->dff_level = L;
     if (h->verbose)
-        fprintf(stderr, "[uno_kkt] dataflow factorization: levels %d..%d, %zu fronts\n", L, S.nlevels - 1, order.size());
+        fprintf(stderr, "[uno_kkt] dataflow factorization: %zu fronts (levels >= %d and fronts <= %d rows below them), "
+                        "%d level launches before\n", order.size(), L, M, (int)h->dff_plan.fac.size());
     return hipSuccess;
 }
 
@@ -960,10 +980,10 @@ int enqueue_factorization(uno_kkt_t h) {
     A.df_order = nullptr; A.df_nf = 0; A.df_nch = nullptr; A.df_cnt = nullptr; A.df_epoch = 0; A.df_abort = nullptr;
     A.df_ticket = nullptr;
     const bool dff = h->dff_level != INT32_MAX;
-    for (const Launch& L : h->plan[0].fac) {
-        if (dff && L.level >= h->dff_level) continue;
+    const Plan& lp = dff ? h->dff_plan : h->plan[0];
+    for (const Launch& L : lp.fac) {
         TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
-        HIPCHK(h, launch_factor(A, h->plan[0].fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+        HIPCHK(h, launch_factor(A, lp.fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
     }
     if (dff) {
         TimerScope t(h, KC_FACTOR_LDS);
@@ -1063,7 +1083,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
     else if (n == "dataflow_factor") {
-        h->dff_enabled = value != 0.0;
+        h->dff_enabled = std::max(0, std::min(2, (int)value));
         if (h->analyzed) {
             HIPCHK(h, setup_factor_dataflow(h));
             HIPCHK(h, hipStreamSynchronize(h->stream));
