@@ -4,8 +4,10 @@
 // factorization the plugin performed.  This is the in-container stand-in for `uno_ampl model.nl -AMPL
 // preset=ipopt linear_solver=HIPLDL` (bindings/AMPL/uno_ampl.cpp:78-139; ASL is not available).
 //
-// usage: uno_kkt_driver <model> [option=value ...]     model: hs015 (hand-coded) or a path to a text .nl file
+// usage: uno_kkt_driver <model> [option=value ...]     model: hs015 (hand-coded), arrowband:<N> (synthetic NLP) or a path to a text .nl file
+#include <cmath>
 #include <cstdio>
+#include <algorithm>
 #include <iostream>
 #include <memory>
 #include <string>
@@ -15,6 +17,7 @@
 #include "model/ModelFactory.hpp"
 #include "models/HS015Model.hpp"
 #include "models/NLModel.hpp"
+#include "models/ArrowbandModel.hpp"
 #include "optimization/Iterate.hpp"
 #include "optimization/Result.hpp"
 #include "options/DefaultOptions.hpp"
@@ -45,6 +48,9 @@ int main(int argc, char* argv[]) {
       if (model_name == "hs015") {
          model = std::make_unique<HS015Model>();
       }
+      else if (model_name.rfind("arrowband:", 0) == 0) {  // synthetic arrowband NLP of KKT dimension N
+         model = std::make_unique<ArrowbandModel>(std::stoul(model_name.substr(10)));
+      }
       else if (model_name.size() > 3 && model_name.compare(model_name.size() - 3, 3, ".nl") == 0) {
          model = std::make_unique<NLModel>(model_name);  // ASL-free .nl reader (models/NLModel.hpp)
       }
@@ -66,9 +72,16 @@ int main(int argc, char* argv[]) {
          model_name.c_str(), options.get_string("linear_solver").c_str(), static_cast<int>(result.optimization_status),
          result.iteration, result.solution.evaluations.objective);
       std::printf(", \"primals\": [");
-      for (size_t i = 0; i < result.number_variables; ++i) {
+      const size_t shown = result.number_variables <= 64 ? result.number_variables : 0;  // large models: summary only
+      for (size_t i = 0; i < shown; ++i) {
          std::printf("%s%.17g", i ? ", " : "", result.solution.primals[i]);
       }
+      double ps = 0., pq = 0., pm = 0.;
+      for (size_t i = 0; i < result.number_variables; ++i) {
+         const double v = result.solution.primals[i];
+         ps += v; pq += v * v; pm = std::max(pm, std::fabs(v));
+      }
+      std::printf("], \"primals_summary\": [%.17g, %.17g, %.17g", ps, pq, pm);
       size_t nf = 0, ns = 0;
       for (const auto& e: kkt_trace::events()) {
          (e.kind == 'F' ? nf : ns)++;

@@ -8,3 +8,6 @@ for m in hs015 polak5; do
   oracle/_ref/uno_kkt_driver tests/golden/$m.nl linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
     | sed "s#\"model\": \"tests/golden/$m.nl\"#\"model\": \"$m.nl\"#" > tests/golden/${m}_nl_uno_oracle.json
 done
+# configs[1]: the synthetic arrowband NLP of KKT dimension 1e4 (integration/models/ArrowbandModel.hpp)
+oracle/_ref/uno_kkt_driver arrowband:10000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
+  > tests/golden/arrowband10000_uno_oracle.json

@@ -103,3 +103,40 @@ def test_hipldl_plugin_nl(model):
     at the optimum, x[2] ~ 6e-3 at termination), so its final value reflects the factorization's
     rounding at ~1e-9: primals within 1e-8 there."""
     same_run(run_nl(model, "HIPLDL"), NL_GOLDEN[model], xtol=1e-10 if model == "hs015" else 1e-8)
+
+
+# ---- configs[1]: a whole ipopt-preset solve of the synthetic arrowband NLP, KKT dimension 1e4 ----
+AB_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "arrowband10000_uno_oracle.json")))
+
+
+def run_model(model, solver):
+    out = subprocess.run([DRIVER, model, f"linear_solver={solver}", "logger=SILENT"], capture_output=True, text=True,
+                         timeout=300)
+    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
+    return json.loads(line)
+
+
+def same_large_run(r, g, rel=1e-10):
+    assert r["status"] == g["status"] == 0
+    assert r["iterations"] == g["iterations"]
+    assert r["factorizations"] == g["factorizations"] and r["solves"] == g["solves"]
+    assert r["inertia_trace"] == g["inertia_trace"]
+    assert abs(r["objective"] - g["objective"]) <= rel * abs(g["objective"])
+    for a, b in zip(r["primals_summary"], g["primals_summary"]):
+        assert abs(a - b) <= 1e-8 * max(1.0, abs(b))
+
+
+@needs_driver
+def test_oracle_plugin_arrowband_c2():
+    """Nonconvex QP (H indefinite, box bounds, 2 500 linear equalities): 159 IPM iterations, 387
+    factorizations of which 227 are inertia-correction retries (PrimalDualRegularization.hpp:133-219)."""
+    same_large_run(run_model("arrowband:10000", "ORACLE"), AB_GOLDEN, rel=0.0)
+
+
+@needs_driver
+@pytest.mark.gpu
+def test_hipldl_plugin_arrowband_c2():
+    """north_star at configs[1]: the GPU plugin inside the reference Uno core gives the oracle's
+    iterate sequence on a 1e4 KKT (iterations, every factorization's inertia, factorization / solve
+    counts identical) and objective within 1e-10 relative."""
+    same_large_run(run_model("arrowband:10000", "HIPLDL"), AB_GOLDEN)
