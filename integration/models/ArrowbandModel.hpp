@@ -32,9 +32,12 @@ namespace uno {
    public:
       static constexpr size_t band = 12, window = 28, arrow = 6;
 
-      explicit ArrowbandModel(size_t N, uint64_t seed = 0x5EED0002ull):
-            Model("arrowband" + std::to_string(N), (3 * N) / 4, N - (3 * N) / 4, 1.),
-            all_collection(this->all), empty_collection(this->empty), equality_collection(this->equalities),
+      // inequality = true: -1 <= A x - b <= 1 instead of A x = b (the ipopt preset adds slacks:
+      // the inequality-constrained KKT structure of SURVEY.md 8(f) item 4's fallback measurement)
+      explicit ArrowbandModel(size_t N, bool inequality = false, uint64_t seed = 0x5EED0002ull):
+            Model((inequality ? "arrowband_ineq" : "arrowband") + std::to_string(N), (3 * N) / 4, N - (3 * N) / 4, 1.),
+            inequality(inequality), all_collection(this->all), empty_collection(this->empty),
+            equality_collection(this->equalities), inequality_collection(this->inequalities),
             linear_constraints(0, N - (3 * N) / 4) {
          const size_t nv = this->number_variables, m = this->number_constraints;
          if (nv < window + arrow + 1 || m < 1) throw std::invalid_argument("arrowband: N too small");
@@ -69,7 +72,7 @@ namespace uno {
             this->b[j] = bj;
          }
          for (size_t i = 0; i < nv; ++i) this->all.push_back(i);
-         for (size_t j = 0; j < m; ++j) this->equalities.push_back(j);
+         for (size_t j = 0; j < m; ++j) (inequality ? this->inequalities : this->equalities).push_back(j);
       }
 
       [[nodiscard]] double evaluate_objective(const Vector<double>& x) const override {
@@ -123,10 +126,10 @@ namespace uno {
       [[nodiscard]] const Collection<size_t>& get_single_lower_bounded_variables() const override { return this->empty_collection; }
       [[nodiscard]] const Collection<size_t>& get_single_upper_bounded_variables() const override { return this->empty_collection; }
       [[nodiscard]] const Vector<size_t>& get_fixed_variables() const override { return this->fixed; }
-      [[nodiscard]] double constraint_lower_bound(size_t) const override { return 0.; }
-      [[nodiscard]] double constraint_upper_bound(size_t) const override { return 0.; }
+      [[nodiscard]] double constraint_lower_bound(size_t) const override { return this->inequality ? -1. : 0.; }
+      [[nodiscard]] double constraint_upper_bound(size_t) const override { return this->inequality ? 1. : 0.; }
       [[nodiscard]] const Collection<size_t>& get_equality_constraints() const override { return this->equality_collection; }
-      [[nodiscard]] const Collection<size_t>& get_inequality_constraints() const override { return this->empty_collection; }
+      [[nodiscard]] const Collection<size_t>& get_inequality_constraints() const override { return this->inequality_collection; }
       [[nodiscard]] const Collection<size_t>& get_linear_constraints() const override { return this->linear_constraints; }
       void initial_primal_point(Vector<double>& x) const override { std::fill(x.begin(), x.begin() + this->number_variables, 0.); }
       void initial_dual_point(Vector<double>& y) const override { std::fill(y.begin(), y.begin() + this->number_constraints, 0.); }
@@ -157,8 +160,9 @@ namespace uno {
       std::vector<size_t> hcol_start;
       std::vector<double> hval, g, b;
       std::vector<std::vector<std::pair<size_t, double>>> rows;
-      std::vector<size_t> all, empty, equalities;
-      CollectionAdapter<std::vector<size_t>&> all_collection, empty_collection, equality_collection;
+      bool inequality;
+      std::vector<size_t> all, empty, equalities, inequalities;
+      CollectionAdapter<std::vector<size_t>&> all_collection, empty_collection, equality_collection, inequality_collection;
       ForwardRange linear_constraints;
       SparseVector<size_t> slacks{};
       Vector<size_t> fixed{};

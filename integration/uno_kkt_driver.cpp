@@ -51,6 +51,9 @@ int main(int argc, char* argv[]) {
       else if (model_name.rfind("arrowband:", 0) == 0) {  // synthetic arrowband NLP of KKT dimension N
          model = std::make_unique<ArrowbandModel>(std::stoul(model_name.substr(10)));
       }
+      else if (model_name.rfind("arrowband_ineq:", 0) == 0) {  // the same with -1 <= A x - b <= 1
+         model = std::make_unique<ArrowbandModel>(std::stoul(model_name.substr(15)), true);
+      }
       else if (model_name.size() > 3 && model_name.compare(model_name.size() - 3, 3, ".nl") == 0) {
          model = std::make_unique<NLModel>(model_name);  // ASL-free .nl reader (models/NLModel.hpp)
       }

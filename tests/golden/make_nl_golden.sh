@@ -11,3 +11,9 @@ done
 # configs[1]: the synthetic arrowband NLP of KKT dimension 1e4 (integration/models/ArrowbandModel.hpp)
 oracle/_ref/uno_kkt_driver arrowband:10000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
   > tests/golden/arrowband10000_uno_oracle.json
+# the inequality-constrained variant (-1 <= A x - b <= 1: slacks in the ipopt preset), SURVEY 8(f) item 4
+oracle/_ref/uno_kkt_driver arrowband_ineq:10000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
+  > tests/golden/arrowband_ineq10000_uno_oracle.json
+# n = 1e5 (4.5 min on one core; compared by the GPU test only)
+oracle/_ref/uno_kkt_driver arrowband:100000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
+  > tests/golden/arrowband100000_uno_oracle.json

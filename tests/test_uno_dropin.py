@@ -107,6 +107,7 @@ def test_hipldl_plugin_nl(model):
 
 # ---- configs[1]: a whole ipopt-preset solve of the synthetic arrowband NLP, KKT dimension 1e4 ----
 AB_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "arrowband10000_uno_oracle.json")))
+ABI_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "arrowband_ineq10000_uno_oracle.json")))
 
 
 def run_model(model, solver):
@@ -140,3 +141,25 @@ def test_hipldl_plugin_arrowband_c2():
     iterate sequence on a 1e4 KKT (iterations, every factorization's inertia, factorization / solve
     counts identical) and objective within 1e-10 relative."""
     same_large_run(run_model("arrowband:10000", "HIPLDL"), AB_GOLDEN)
+
+
+@needs_driver
+def test_oracle_plugin_arrowband_inequalities():
+    """Inequality-constrained variant (-1 <= A x - b <= 1): the ipopt preset adds 2 500 slacks
+    (KKT dimension 12 500); 181 iterations, 440 factorizations."""
+    same_large_run(run_model("arrowband_ineq:10000", "ORACLE"), ABI_GOLDEN, rel=0.0)
+
+
+@needs_driver
+@pytest.mark.gpu
+def test_hipldl_plugin_arrowband_inequalities():
+    same_large_run(run_model("arrowband_ineq:10000", "HIPLDL"), ABI_GOLDEN)
+
+
+@needs_driver
+@pytest.mark.gpu
+def test_hipldl_plugin_arrowband_1e5():
+    """KKT dimension 1e5 (golden: the ORACLE run, 310 iterations, 759 factorizations, 4.5 min on one
+    core; tests/golden/make_nl_golden.sh): identical iteration / factorization sequence on the GPU."""
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "arrowband100000_uno_oracle.json")))
+    same_large_run(run_model("arrowband:100000", "HIPLDL"), g)
