@@ -103,6 +103,10 @@ struct uno_kkt {
     // threshold 0 and records its smallest accepted pivot; finish_factorization checks it against the
     // exact threshold and refactors with the exact one in the (rare) case it would have mattered
     hipStream_t stream2 = nullptr;
+    // the size-class launches of one factorization level are independent: the second and later run on
+    // stream3 beside the first (fork / join events), so one launch's tail overlaps the other's body
+    hipStream_t stream3 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     hipEvent_t ev_scale = nullptr, ev_norm = nullptr;
     int overlap_norm = 1;
     bool exact_next = false, last_optimistic = false;
@@ -151,6 +155,7 @@ struct uno_kkt {
     DBuf<unsigned long long> df_stamps;
     // dataflow factorization of the upper tree (levels >= dff_level, every front one-wave); option
     // "dataflow_factor" (default 1)
+    int concurrent_classes = 1;  // option "concurrent_classes"
     int dff_enabled = 1;  // 0 off, 1 (default) levels >= L*, 2 also the small fronts below them (measured no faster at C3)
     int dff_level = INT32_MAX;     // first level of the dataflow launch (INT32_MAX: none)
     int dff_mmax = 0;
@@ -981,9 +986,24 @@ int enqueue_factorization(uno_kkt_t h) {
     A.df_ticket = nullptr;
     const bool dff = h->dff_level != INT32_MAX;
     const Plan& lp = dff ? h->dff_plan : h->plan[0];
-    for (const Launch& L : lp.fac) {
-        TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
-        HIPCHK(h, launch_factor(A, lp.fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+    for (size_t q = 0; q < lp.fac.size();) {
+        size_t r = q + 1;  // launches [q, r) of one level
+        while (r < lp.fac.size() && lp.fac[r].level == lp.fac[q].level) ++r;
+        TimerScope t(h, lp.fac[q].global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
+        if (r - q > 1 && h->concurrent_classes) {
+            HIPCHK(h, hipEventRecord(h->ev_fork, s));
+            HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork, 0));
+        }
+        for (size_t u = q; u < r; ++u) {
+            const Launch& L = lp.fac[u];
+            hipStream_t ls = (u > q && h->concurrent_classes) ? h->stream3 : s;
+            HIPCHK(h, launch_factor(A, lp.fac_fronts.p + L.begin, L.count, L.mmax, L.global, ls));
+        }
+        if (r - q > 1 && h->concurrent_classes) {
+            HIPCHK(h, hipEventRecord(h->ev_join, h->stream3));
+            HIPCHK(h, hipStreamWaitEvent(s, h->ev_join, 0));
+        }
+        q = r;
     }
     if (dff) {
         TimerScope t(h, KC_FACTOR_LDS);
@@ -1038,6 +1058,9 @@ int uno_kkt_create(uno_kkt_t* handle, int device_id) {
     h->device = device_id;
     if (hipSetDevice(device_id) != hipSuccess || hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
         hipStreamCreateWithFlags(&h->stream2, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithFlags(&h->stream3, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_scale, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_norm, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counters, 12 * sizeof(unsigned long long)) != hipSuccess) {
@@ -1060,6 +1083,9 @@ void uno_kkt_destroy(uno_kkt_t h) {
     if (h->ev_scale) hipEventDestroy(h->ev_scale);
     if (h->ev_norm) hipEventDestroy(h->ev_norm);
     if (h->stream2) hipStreamDestroy(h->stream2);
+    if (h->stream3) { hipStreamSynchronize(h->stream3); hipStreamDestroy(h->stream3); }
+    if (h->ev_fork) hipEventDestroy(h->ev_fork);
+    if (h->ev_join) hipEventDestroy(h->ev_join);
     delete h->comm;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -1082,6 +1108,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "verbose") h->verbose = (int)value;
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
+    else if (n == "concurrent_classes") h->concurrent_classes = value != 0.0;
     else if (n == "dataflow_factor") {
         h->dff_enabled = std::max(0, std::min(2, (int)value));
         if (h->analyzed) {
