@@ -5,6 +5,7 @@
 // preset=ipopt linear_solver=HIPLDL` (bindings/AMPL/uno_ampl.cpp:78-139; ASL is not available).
 //
 // usage: uno_kkt_driver <model> [option=value ...]     model: hs015 (hand-coded), arrowband:<N> (synthetic NLP) or a path to a text .nl file
+//        uno_kkt_driver convexify:<model> [option=value ...]   byrd-preset Hessian convexification only (see below)
 #include <cmath>
 #include <cstdio>
 #include <algorithm>
@@ -18,29 +19,97 @@
 #include "models/HS015Model.hpp"
 #include "models/NLModel.hpp"
 #include "models/ArrowbandModel.hpp"
+#include "ingredients/constraint_relaxation_strategies/l1RelaxedProblem.hpp"
+#include "ingredients/hessian_models/HessianModel.hpp"
+#include "ingredients/hessian_models/HessianModelFactory.hpp"
+#include "ingredients/regularization_strategies/PrimalRegularization.hpp"
+#include "linear_algebra/COOFormat.hpp"
+#include "linear_algebra/SparseSymmetricMatrix.hpp"
 #include "optimization/Iterate.hpp"
+#include "optimization/Multipliers.hpp"
 #include "optimization/Result.hpp"
 #include "options/DefaultOptions.hpp"
 #include "options/Options.hpp"
 #include "options/Presets.hpp"
 #include "tools/Logger.hpp"
+#include "tools/Statistics.hpp"
 #include "tools/UserCallbacks.hpp"
 
 using namespace uno;
+
+// The byrd preset's use of the plugin: Hessian convexification by
+// PrimalRegularization::regularize_hessian (PrimalRegularization.hpp:79-129) of the l1-relaxed problem's
+// Lagrangian Hessian, exactly as Subproblem::compute_regularized_hessian (Subproblem.cpp:32-43) drives it
+// from BQPD's Hessian callback (BQPDSolver.cpp:89-96, 405-407).  BQPD itself is absent (proprietary), so the
+// QP iterations cannot run; instead the Hessian is convexified at a fixed sequence of primal-dual points and
+// penalty parameters, reusing ONE PrimalRegularization instance (one symbolic analysis, as in a solve).
+// Expected inertia (n_model, 0, n_elastic): the elastic variables have empty Hessian rows (null pivots).
+static void run_convexification(const Model& model, const Options& options) {
+   const auto hessian_model = HessianModelFactory::create(options);
+   const double coefficient = options.get_double("l1_constraint_violation_coefficient");
+   const l1RelaxedProblem shape(model, 1., coefficient);
+   const size_t n = shape.number_variables, n_model = model.number_variables;
+   const size_t regularization_size = shape.get_number_original_variables();  // InequalityConstrainedMethod.cpp:28-29
+   SparseSymmetricMatrix<COOFormat<size_t, double>> hessian(n, shape.number_hessian_nonzeros(*hessian_model), regularization_size);
+   PrimalRegularization<double> regularization(options);
+   Statistics statistics;
+   regularization.initialize_statistics(statistics, options);
+   regularization.initialize_memory(shape, *hessian_model);
+   Vector<double> x0(n, 0.), x(n, 0.);
+   Vector<double> y0(model.number_constraints, 0.);
+   model.initial_primal_point(x0);
+   model.project_onto_variable_bounds(x0);
+   model.initial_dual_point(y0);
+   const double rhos[] = {1., 0.1, 1e-2, 1., 10., 1e-3};
+   std::printf("{\"mode\": \"convexify\", \"linear_solver\": \"%s\", \"dimension\": %zu, \"model_variables\": %zu, \"points\": [",
+      options.get_string("linear_solver").c_str(), n, n_model);
+   for (size_t k = 0; k < sizeof(rhos) / sizeof(rhos[0]); ++k) {
+      // deterministic primal-dual points around the initial point
+      for (size_t i = 0; i < n; ++i) {
+         x[i] = (i < n_model ? x0[i] : 0.) + 0.25 * static_cast<double>(k) * std::sin(1.7 * static_cast<double>(i) + 1.);
+      }
+      model.project_onto_variable_bounds(x);
+      Multipliers multipliers(n, model.number_constraints);
+      for (size_t j = 0; j < model.number_constraints; ++j) {
+         multipliers.constraints[j] = y0[j] + 0.5 * static_cast<double>(k) * std::cos(1.3 * static_cast<double>(j) + 0.5);
+      }
+      const l1RelaxedProblem problem(model, rhos[k], coefficient);
+      const size_t before = kkt_trace::events().size();
+      hessian.reset();
+      problem.evaluate_lagrangian_hessian(statistics, *hessian_model, x, multipliers, hessian);
+      const Inertia expected_inertia{problem.get_number_original_variables(), 0, n - problem.get_number_original_variables()};
+      double smallest = hessian.smallest_diagonal_entry(expected_inertia.positive);
+      regularization.regularize_hessian(statistics, hessian, problem.get_primal_regularization_variables(), expected_inertia);
+      std::printf("%s{\"rho\": %.17g, \"smallest_diagonal_entry\": %.17g, \"regularization\": %.17g, \"factorizations\": %zu}",
+         k ? ", " : "", rhos[k], smallest, regularization.get_primal_regularization_factor(), kkt_trace::events().size() - before);
+   }
+   std::printf("], \"inertia_trace\": [");
+   bool first = true;
+   for (const auto& e: kkt_trace::events()) {
+      if (e.kind != 'F') continue;
+      std::printf("%s[%zu, %lld, %lld, %lld]", first ? "" : ", ", e.dimension, static_cast<long long>(e.positive),
+         static_cast<long long>(e.negative), static_cast<long long>(e.zero));
+      first = false;
+   }
+   std::printf("]}\n");
+}
 
 int main(int argc, char* argv[]) {
    if (argc < 2) {
       std::cerr << "usage: " << argv[0] << " hs015 [option=value ...]\n";
       return 2;
    }
-   const std::string model_name = argv[1];
+   std::string model_name = argv[1];
+   const bool convexify = model_name.rfind("convexify:", 0) == 0;
+   if (convexify) model_name = model_name.substr(10);
    try {
       // option precedence of uno_ampl.cpp:106-128: defaults -> solvers -> preset -> command line
       Options options = DefaultOptions::load();
       options.overwrite_with(DefaultOptions::determine_solvers());
       Options command_line = Options::get_command_line_options(argc, argv, 2);
       const auto preset = command_line.get_string_optional("preset");
-      options.overwrite_with(Presets::get_preset_options(preset.has_value() ? preset : std::optional<std::string>("ipopt")));
+      options.overwrite_with(Presets::get_preset_options(preset.has_value() ? preset :
+         std::optional<std::string>(convexify ? "byrd" : "ipopt")));
       options.overwrite_with(command_line);
       Logger::set_logger(options.get_string("logger"));
 
@@ -59,6 +128,10 @@ int main(int argc, char* argv[]) {
       }
       else {
          throw std::invalid_argument("unknown model " + model_name);
+      }
+      if (convexify) {
+         run_convexification(*model, options);
+         return 0;
       }
       model = ModelFactory::reformulate(std::move(model), options);
       Iterate initial_iterate(model->number_variables, model->number_constraints);

@@ -17,3 +17,15 @@ oracle/_ref/uno_kkt_driver arrowband_ineq:10000 linear_solver=ORACLE logger=SILE
 # n = 1e5 (4.5 min on one core; compared by the GPU test only)
 oracle/_ref/uno_kkt_driver arrowband:100000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
   > tests/golden/arrowband100000_uno_oracle.json
+# byrd-preset Hessian convexification (PrimalRegularization::regularize_hessian on the l1-relaxed problem's
+# Hessian at a fixed sequence of points; driver mode convexify:<model>)
+python3 - <<'PY'
+import json, subprocess
+out = {}
+for m in ("tests/golden/hs015.nl", "tests/golden/polak5.nl", "arrowband:10000", "arrowband_ineq:10000", "arrowband:100000",
+          "arrowband:1000000"):
+    r = subprocess.run(["oracle/_ref/uno_kkt_driver", "convexify:" + m, "linear_solver=ORACLE", "logger=SILENT"],
+                       capture_output=True, text=True, check=True)
+    out[m.replace("tests/golden/", "")] = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+json.dump(out, open("tests/golden/convexify_uno_oracle.json", "w"), indent=0)
+PY

@@ -163,3 +163,51 @@ def test_hipldl_plugin_arrowband_1e5():
     core; tests/golden/make_nl_golden.sh): identical iteration / factorization sequence on the GPU."""
     g = json.load(open(os.path.join(ROOT, "tests", "golden", "arrowband100000_uno_oracle.json")))
     same_large_run(run_model("arrowband:100000", "HIPLDL"), g)
+
+
+# ---- byrd preset: Hessian convexification (SURVEY.md 8(f) item 3) ----
+CVX_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "convexify_uno_oracle.json")))
+
+
+def run_convexify(model, solver):
+    path = os.path.join(ROOT, "tests", "golden", model) if model.endswith(".nl") else model
+    out = subprocess.run([DRIVER, "convexify:" + path, f"linear_solver={solver}", "logger=SILENT"], capture_output=True,
+                         text=True, timeout=600)
+    return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+
+
+def same_convexification(r, g):
+    """PrimalRegularization.hpp:79-129 driven by the plugin: identical factorization count per point, every
+    inertia identical, identical regularization factor (the factor sequence is decided by the inertias)."""
+    assert r["dimension"] == g["dimension"]
+    assert r["inertia_trace"] == g["inertia_trace"]
+    assert [(p["rho"], p["regularization"], p["factorizations"]) for p in r["points"]] == \
+           [(p["rho"], p["regularization"], p["factorizations"]) for p in g["points"]]
+
+
+def test_convexify_golden_semantics():
+    """Each point ends with the expected inertia (n_model, 0, n_elastic): elastic rows are empty (null pivots)."""
+    for g in CVX_GOLDEN.values():
+        n, nm = g["dimension"], g["model_variables"]
+        ends = []
+        k = 0
+        for p in g["points"]:
+            k += p["factorizations"]
+            ends.append(g["inertia_trace"][k - 1])
+        assert k == len(g["inertia_trace"])
+        assert all(e[1:] == [nm, 0, n - nm] for e in ends), ends
+
+
+@needs_driver
+@pytest.mark.parametrize("model", ["hs015.nl", "polak5.nl", "arrowband:10000", "arrowband_ineq:10000"])
+def test_oracle_plugin_convexify(model):
+    same_convexification(run_convexify(model, "ORACLE"), CVX_GOLDEN[model])
+
+
+@needs_driver
+@pytest.mark.gpu
+@pytest.mark.parametrize("model", list(CVX_GOLDEN))
+def test_hipldl_plugin_convexify(model):
+    """The GPU plugin under the byrd preset's convexification loop (up to dimension 1.25e6 with 5e5 empty
+    elastic rows) reproduces the oracle's inertia and regularization sequence."""
+    same_convexification(run_convexify(model, "HIPLDL"), CVX_GOLDEN[model])
