@@ -212,3 +212,21 @@ def test_dataflow_matches_level_schedule(uno_amd, n):
     b2 = np.cos(np.arange(N))
     np.testing.assert_array_equal(gd.solve(b2), gl.solve(b2))
     assert gd.stats()["solve_aborts"] == 0 and gd.stats()["factor_df_aborts"] == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("window", [74, 160, 400])
+def test_dataflow_panel_windows(uno_amd, window):
+    """Panels larger than the LDS window are solved in column windows (forward first to last, backward
+    last to first, later windows loaded from L): bit-identical to the level schedule, with 2x2 pivots."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    N, nv, m, r, c, v, b = arrowband(20000, SEEDS["C2"])
+    gd, gl = HipKKT(0, solve_window=window), HipKKT(0, dataflow_solve=0)
+    for g in (gd, gl):
+        g.analyze(N, r, c)
+        g.factorize(v)
+    assert gd.inertia() == gl.inertia()
+    assert gd.stats()["pivots_2x2"] > 0
+    for rep in range(2):
+        np.testing.assert_array_equal(gd.solve(b * (rep + 1)), gl.solve(b * (rep + 1)))
+    assert gd.stats()["solve_aborts"] == 0

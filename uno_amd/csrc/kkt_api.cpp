@@ -143,6 +143,7 @@ struct uno_kkt {
     // one-wave eligible; option "dataflow_solve" (default 1)
     int df_enabled = 1;
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
+    int df_win = 0, df_win_opt = 0; // LDS panel window of the dataflow solve (option solve_window, 0 = auto)
     uint32_t df_epoch = 0;
     bool df_rx_valid = false;      // rxpos matches the last factorization's pivoting
     bool df_check = false;         // a dataflow solve's abort flag copy is pending
@@ -255,6 +256,7 @@ DfArgs dataflow_args(uno_kkt_t h) {
     D.done = h->df_done.p; D.epoch = h->df_epoch; D.cvx = h->df_cvx.p; D.cvx_off = h->df_cvx_off.p;
     D.ch_cvx_off = h->df_ch_cvx_off.p; D.xs = h->df_xs.p; D.xs_off = h->df_xs_off.p; D.rxpos = h->df_rxpos.p;
     D.abort_flag = h->df_abort.p;
+    D.win = h->df_win;
     D.stamps = h->want_solve_stamps ? h->df_stamps.p : nullptr;
     return D;
 }
@@ -738,16 +740,25 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     h->df_rx_valid = false;
     h->df_epoch = 0;
     if (h->world > 1 || !h->df_enabled || S.nf == 0) return hipSuccess;
-    int lds = 0;
+    int max_sz = 0, mmax = 0;
     for (int64_t f = 0; f < S.nf; ++f) {
         const int m = S.f_m[f], p = S.f_p[f];
         if (p > 64 || m > kMaxLdsFront) {  // a front needs the 256-thread kernels
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve off: front %lld m %d p %d\n", (long long)f, m, p);
             return hipSuccess;
         }
-        const int sz = p * m - p * (p - 1) / 2;
-        lds = std::max(lds, ((sz + 1) & ~1) + ((m + 1) & ~1) + (m + 1) / 2);
+        max_sz = std::max(max_sz, p * m - p * (p - 1) / 2);
+        mmax = std::max(mmax, m);
     }
+    // panel window: sized so that 16 one-wave blocks (4 per SIMD, the register limit of the dataflow
+    // kernels) fit the 160 KB LDS of a CU; larger panels are processed in column windows
+    const int rows_lds = ((mmax + 1) & ~1) + (mmax + 1) / 2;
+    int win = h->df_win_opt > 0 ? h->df_win_opt : (160 * 1024 / 16 - 16) / 8 - solve_slack_doubles() - rows_lds;
+    win = std::max(win, mmax + 1) & ~1;
+    win = std::min(win, (max_sz + 1) & ~1);
+    win = std::max(win, 2);
+    h->df_win = win;
+    const int lds = win + rows_lds;
     std::vector<int64_t> cvx(S.nf), xs(S.nf), chx(S.child.size());
     int64_t tc = 0, tx = 0;
     for (int64_t f = 0; f < S.nf; ++f) {
@@ -789,7 +800,9 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     if ((e = hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     h->df_lds = lds;
     h->df_grid = solve_df_grid(lds, (int)S.nf);
-    if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve: %lld fronts, lds %d doubles, grid %d\n", (long long)S.nf, lds, h->df_grid);
+    if (h->verbose)
+        fprintf(stderr, "[uno_kkt] dataflow solve: %lld fronts, panel window %d of %d doubles, lds %d doubles, grid %d\n",
+                (long long)S.nf, win, max_sz, lds, h->df_grid);
     return hipSuccess;
 }
 
@@ -1113,6 +1126,13 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
         h->dff_enabled = std::max(0, std::min(2, (int)value));
         if (h->analyzed) {
             HIPCHK(h, setup_factor_dataflow(h));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+    }
+    else if (n == "solve_window") {
+        h->df_win_opt = std::max(0, (int)value);
+        if (h->analyzed) {
+            HIPCHK(h, setup_dataflow(h));
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }

@@ -1352,6 +1352,7 @@ __device__ __forceinline__ int pcol(int m, int k) { return k * m - k * (k - 1) /
 
 // Panel -> LDS: 16-byte loads (after one leading double when the panel starts on an odd double), up
 // to 16 per lane issued before the first LDS write.
+template <int B = 16>
 __device__ __forceinline__ void stage_panel(const double* __restrict__ L, int64_t Lo, int sz, double* P) {
     const int lane = threadIdx.x;
     const int head = (int)(Lo & 1) < sz ? (int)(Lo & 1) : sz;
@@ -1360,7 +1361,7 @@ __device__ __forceinline__ void stage_panel(const double* __restrict__ L, int64_
     if (((sz - head) & 1) && lane == 0) P[sz - 1] = L[Lo + sz - 1];
     if (npair <= 0) return;
     const double2* L2 = reinterpret_cast<const double2*>(L + Lo + head);
-    constexpr int B = 16;
+    
     for (int t0 = 0; t0 < npair; t0 += B * 64) {
         double2 v[B];
 #pragma unroll
@@ -1569,7 +1570,20 @@ __global__ __launch_bounds__(64) void k_solve_bwd_w(SolveArgs A, const int32_t* 
 // solution gathered out by k_xs_in / k_xs_out), so a front's own values need no row-id round trip.
 // A front then costs one dependent round trip (its children's / ancestors' values), its arithmetic
 // and the store drain before its signal.
-constexpr int kPre = 16;
+__device__ __forceinline__ int col_start(int m, int k) { return k * m - k * (k - 1) / 2; }  // flat index of L(k, k)
+__device__ __forceinline__ int fwd_chunk_end(int m, int p, int k0, int win) {
+    int k1 = k0, used = 0;
+    while (k1 < p && used + (m - k1) <= win) { used += m - k1; ++k1; }
+    return k1 > k0 ? k1 : k0 + 1;
+}
+__device__ __forceinline__ int bwd_chunk_begin(int m, int p, int c1, int win) {
+    const int e1 = col_start(m, c1);
+    int c0 = c1;
+    while (c0 > 0 && e1 - col_start(m, c0 - 1) <= win) --c0;
+    return c0 < c1 ? c0 : c1 - 1;
+}
+
+constexpr int kPre = 8;  // 1 024 doubles: the default panel window (solve_window) fits
 struct FrontRec {
     int f, m, p, sz, par, c0, c1;
     int64_t ro, Lo;
@@ -1578,6 +1592,8 @@ struct FrontRec {
 };
 struct FrontPre {
     FrontRec r;
+    int w0, wlen;      // the prefetched window: flat panel range [w0, w0 + wlen), its first column window
+    int kw;            // forward: end column of that window; backward: its first column
     int head, npair;
     int mypiv;
     int32_t a0, a1;    // backward: xs index (rxpos) of the contribution rows lane, lane + 64 (>= p)
@@ -1637,12 +1653,23 @@ __device__ __forceinline__ void df_issue(const SolveArgs& A, const DfArgs& D, Fr
         q.a1 = lane + 64 < m && lane + 64 >= p ? D.rxpos[ro + lane + 64] : 0;
         q.dep = q.r.par >= 0 ? ld_sc1_u32(D.done + q.r.par) : 0u;
     }
-    q.head = (int)(q.r.Lo & 1) < q.r.sz ? (int)(q.r.Lo & 1) : q.r.sz;
-    q.npair = (q.r.sz - q.head) >> 1;
-    const double2* L2 = reinterpret_cast<const double2*>(A.L + q.r.Lo + q.head);
+    // first column window of the walk: forward columns [0, kw), backward columns [kw, p)
+    if (FWD) {
+        q.kw = fwd_chunk_end(m, p, 0, D.win);
+        q.w0 = 0;
+        q.wlen = col_start(m, q.kw);
+    } else {
+        q.kw = bwd_chunk_begin(m, p, p, D.win);
+        q.w0 = col_start(m, q.kw);
+        q.wlen = q.r.sz - q.w0;
+    }
+    const int64_t Lw = q.r.Lo + q.w0;
+    q.head = (int)(Lw & 1) < q.wlen ? (int)(Lw & 1) : q.wlen;
+    q.npair = (q.wlen - q.head) >> 1;
+    const double2* L2 = reinterpret_cast<const double2*>(A.L + Lw + q.head);
     const int last = q.npair > 0 ? q.npair - 1 : 0;
-    q.hv = q.head ? A.L[q.r.Lo] : 0.0;
-    q.tv = ((q.r.sz - q.head) & 1) ? A.L[q.r.Lo + q.r.sz - 1] : 0.0;
+    q.hv = q.head ? A.L[Lw] : 0.0;
+    q.tv = ((q.wlen - q.head) & 1) ? A.L[Lw + q.wlen - 1] : 0.0;
 #pragma unroll
     for (int u = 0; u < kPre; ++u) {
         const int t = u * 64 + lane;
@@ -1650,11 +1677,18 @@ __device__ __forceinline__ void df_issue(const SolveArgs& A, const DfArgs& D, Fr
     }
 }
 
-// prefetched panel -> LDS (plus the rare remainder beyond the prefetch, loaded here)
-__device__ __forceinline__ void df_stage(const SolveArgs& A, const FrontPre& q, double* P) {
+// ---- panel window (DfArgs::win doubles of LDS) ----
+// A front's packed panel is staged in column windows of at most `win` doubles, so the LDS per block
+// is sized for the window, not for the largest panel, and more blocks fit a CU (the dataflow solve is
+// bound by the number of fronts in flight).  Most panels fit one window; a larger one is processed in
+// column chunks (forward: first to last, backward: last to first), its later chunks loaded from L.
+// The arithmetic per lane is the same sequence of operations as fwd_compute / bwd_compute, so the
+// windowed solve is bit-identical to the level schedule.
+// the prefetched first window -> P[0 .. wlen) (plus the remainder beyond the prefetch, loaded here)
+__device__ __forceinline__ void df_stage_window(const SolveArgs& A, const FrontPre& q, double* P) {
     const int lane = threadIdx.x;
     if (q.head && lane == 0) P[0] = q.hv;
-    if (((q.r.sz - q.head) & 1) && lane == 0) P[q.r.sz - 1] = q.tv;
+    if (((q.wlen - q.head) & 1) && lane == 0) P[q.wlen - 1] = q.tv;
 #pragma unroll
     for (int u = 0; u < kPre; ++u) {
         const int t = u * 64 + lane;
@@ -1664,7 +1698,7 @@ __device__ __forceinline__ void df_stage(const SolveArgs& A, const FrontPre& q, 
         }
     }
     if (q.npair > kPre * 64) {
-        const double2* L2 = reinterpret_cast<const double2*>(A.L + q.r.Lo + q.head);
+        const double2* L2 = reinterpret_cast<const double2*>(A.L + q.r.Lo + q.w0 + q.head);
         for (int t = kPre * 64 + lane; t < q.npair; t += 64) {
             const double2 v = L2[t];
             P[q.head + 2 * t] = v.x;
@@ -1673,10 +1707,114 @@ __device__ __forceinline__ void df_stage(const SolveArgs& A, const FrontPre& q, 
     }
 }
 
+// fwd_compute over column windows: columns [0, k1) are staged at P on entry.  The diagonal blocks are
+// captured from the operand reads (lane k at step k: L(k,k); lane k+1: L(k+1,k)) instead of being
+// re-read from the panel after the loop.
+__device__ __forceinline__ void fwd_compute_win(const double* __restrict__ L, int64_t Lo, int m, int p, double* P, int win,
+                                                int k1, double* y, int mypiv, double* zdst, double* cvo) {
+    const int lane = threadIdx.x;
+    const bool tri = lane < p;
+    const bool two = m - p > 64;  // uniform
+    double yi = tri ? y[lane] : 0.0;
+    double a0 = p + lane < m ? y[p + lane] : 0.0;
+    double a1 = two && p + 64 + lane < m ? y[p + 64 + lane] : 0.0;
+    double dg = 0.0, sb = 0.0;
+    int pc = 0, base = 0, k = 0;
+    for (;;) {
+        for (; k < k1; ++k) {
+            const int o = pc - base;
+            const double lt = P[max(o + lane, 0)], l0 = P[o + p + lane];
+            const double l1 = two ? P[o + p + 64 + lane] : 0.0;
+            const int kind = __builtin_amdgcn_readlane(mypiv, k);
+            const bool live = kind == PIV_1X1 || kind == PIV_2X2_A || kind == PIV_2X2_B;
+            const double yk = live ? readlane_d(yi, k) : 0.0;
+            const int lim = kind == PIV_2X2_A ? k + 1 : k;
+            const double t = yi - lt * yk;
+            yi = (tri && lane > lim) ? t : yi;
+            a0 -= l0 * yk;
+            a1 -= l1 * yk;
+            dg = lane == k ? lt : dg;
+            sb = lane == k + 1 ? lt : sb;
+            pc += m - k - 1;
+        }
+        if (k >= p) break;
+        base = col_start(m, k);
+        k1 = fwd_chunk_end(m, p, k, win);
+        __syncthreads();
+        stage_panel<4>(L, Lo + base, col_start(m, k1) - base, P);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window's loads are all consumed here, so the
+                                              // operand loop below carries no pending global load
+        __syncthreads();
+    }
+    if (p + lane < m) st_sc1(cvo + lane, a0);
+    if (two && p + 64 + lane < m) st_sc1(cvo + 64 + lane, a1);
+    if (tri) y[lane] = yi;
+    const double dgn = __shfl(dg, lane < 63 ? lane + 1 : lane), sbn = __shfl(sb, lane < 63 ? lane + 1 : lane);
+    const double dgp = __shfl(dg, lane > 0 ? lane - 1 : 0);
+    __syncthreads();  // y of the 2x2 partners below
+    if (tri) {
+        const int kind = mypiv;
+        double out = 0.0;  // null pivot contributes 0
+        if (kind == PIV_1X1) {
+            out = yi / dg;
+        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+            const bool first = kind == PIV_2X2_A;
+            const int k0 = first ? lane : lane - 1;
+            const double a = first ? dg : dgp, b = first ? sbn : sb, e = first ? dgn : dg;
+            const double det = a * e - b * b;
+            const double y0 = y[k0], y1 = y[k0 + 1];
+            out = first ? (e * y0 - b * y1) / det : (a * y1 - b * y0) / det;
+        }
+        *zdst = out;
+    }
+}
+
+// bwd_compute over column windows, last window first: columns [c0, p) are staged at P on entry.  A
+// lane's updates keep their order (rectangle, then k = p-1 .. lane+1): in window [c0, c1) the lanes of
+// the window take the steps k >= c1 with the final x_k of the later windows' lanes, then their own.
+__device__ __forceinline__ double bwd_compute_win(const double* __restrict__ L, int64_t Lo, int m, int p, double* P, int win,
+                                                  int c0, const double* x, int mypiv) {
+    const int lane = threadIdx.x;
+    const bool tri = lane < p;
+    const bool live = tri && mypiv != PIV_NULL;
+    double xj = tri ? x[lane] : 0.0;
+    int c1 = p, base = col_start(m, c0);
+    for (;;) {
+        const bool mine = lane >= c0 && lane < c1;
+        const double* pk = P + (pcol(m, mine ? lane : c0) - base);  // pk[i] = L(i, lane), i >= lane
+        double s0 = 0.0, s1 = 0.0;
+        int i = p;
+        for (; i + 1 < m; i += 2) {
+            s0 += pk[i] * x[i];
+            s1 += pk[i + 1] * x[i + 1];
+        }
+        if (i < m) s0 += pk[i] * x[i];
+        if (live && mine) xj -= s0 + s1;
+        for (int k = p - 1; k >= c0; --k) {
+            const double l = pk[k];
+            const int kind = __builtin_amdgcn_readlane(mypiv, k);
+            const double xk = kind != PIV_NULL ? readlane_d(xj, k) : 0.0;
+            const int skip = kind == PIV_2X2_B ? k - 1 : -1;
+            const double t = xj - l * xk;
+            xj = (live && mine && lane < k && lane != skip) ? t : xj;
+        }
+        if (c0 == 0) break;
+        c1 = c0;
+        c0 = bwd_chunk_begin(m, p, c1, win);
+        base = col_start(m, c0);
+        __syncthreads();
+        stage_panel<4>(L, Lo + base, col_start(m, c1) - base, P);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window's loads are all consumed here, so the
+                                              // operand loop below carries no pending global load
+        __syncthreads();
+    }
+    return xj;
+}
+
 // The walk keeps ONE FrontPre: once a front's prefetched data is consumed (staged into LDS, its
 // scalars copied), the next front's loads are issued into the same registers, so no register copy of
 // an in-flight load (which would wait for it) is needed across iterations.
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_solve_fwd_df(SolveArgs A, DfArgs D) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_fwd_df(SolveArgs A, DfArgs D) {
     extern __shared__ __attribute__((aligned(16))) double smem_s[];
     const int lane = threadIdx.x;
     int t = blockIdx.x;
@@ -1701,8 +1839,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f : nullptr;
         if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
         double* P = smem_s;
-        double* y = smem_s + ((q.r.sz + 1) & ~1);
+        double* y = smem_s + D.win;
         int32_t* fpl = (int32_t*)(y + ((m + 1) & ~1));  // this front's rows were permuted by pivoting
+        const int k1 = q.kw;
+        const int64_t Lo = q.r.Lo;
         if (lane < m) { y[lane] = q.e0; fpl[lane] = q.fp0; }
         if (lane + 64 < m) { y[lane + 64] = 0.0; fpl[lane + 64] = q.fp1; }
         const uint32_t target = D.epoch * (uint32_t)(q.r.c1 - q.r.c0);
@@ -1710,7 +1850,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
             signal();
             df_wait(D.cnt + f, target, D.abort_flag);
         }
-        df_stage(A, q, P);
+        df_stage_window(A, q, P);
         __syncthreads();
         fwd_extend_add<true>(A, D, q.r.c0, q.r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
         __syncthreads();
@@ -1719,7 +1859,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         q.r = df_record(dn);
         df_issue<true>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
-        fwd_compute<true>(m, p, P, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
+        fwd_compute_win(A.L, Lo, m, p, P, D.win, k1, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         pend = par;
         __syncthreads();  // LDS reused by the next front
@@ -1727,7 +1867,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     signal();
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_solve_bwd_df(SolveArgs A, DfArgs D) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_bwd_df(SolveArgs A, DfArgs D) {
     extern __shared__ __attribute__((aligned(16))) double smem_s[];
     const int lane = threadIdx.x;
     int t = blockIdx.x;
@@ -1749,7 +1889,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f + 4 : nullptr;
         if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
         double* P = smem_s;
-        double* x = smem_s + ((q.r.sz + 1) & ~1);
+        double* x = smem_s + D.win;
+        const int c0 = q.kw;
+        const int64_t Lo = q.r.Lo;
         // own pivots: z of the forward solve; contribution rows: the ancestors' published solution
         // values (this launch), through the per-row slot index rxpos, once the parent has published
         if (q.r.par >= 0 && (int32_t)(q.dep - D.epoch) < 0) {
@@ -1758,14 +1900,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         }
         if (lane < m) x[lane] = lane < p ? q.e0 : ld_sc1(D.xs + q.a0);
         if (lane + 64 < m) x[lane + 64] = ld_sc1(D.xs + q.a1);
-        df_stage(A, q, P);
+        df_stage_window(A, q, P);
         __syncthreads();
         signal();
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
         q.r = df_record(dn);
         df_issue<false>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
-        const double xj = bwd_compute(m, p, P, x, mypiv);
+        const double xj = bwd_compute_win(A.L, Lo, m, p, P, D.win, c0, x, mypiv);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (lane < p) st_sc1(D.xs + woff + lane, xj);
         pend = f;
@@ -2006,6 +2148,8 @@ hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax), s, A);
     return hipGetLastError();
 }
+
+int solve_slack_doubles() { return kSolveSlack; }
 
 int solve_df_grid(int lds_doubles, int nf) {
     const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;

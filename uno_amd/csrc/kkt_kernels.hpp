@@ -92,6 +92,7 @@ struct DfArgs {
     const int64_t* xs_off;      // per front
     const int32_t* rxpos;       // per front row (layout of frow): xs index of the rows >= p
     uint32_t* abort_flag;       // set when a wait exceeded its limit (result invalid, host falls back)
+    int32_t win;                // LDS panel window (doubles, even, >= the longest column); rows follow it
     unsigned long long* stamps; // diagnostics (nullptr in normal runs): per front and direction 4 s_memrealtime
                                 // words {start, dependency satisfied, values staged, published}
 };
@@ -164,6 +165,7 @@ hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, in
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
 // dataflow solve: one resident grid of one-wave blocks per direction (grid from the occupancy query)
 int solve_df_grid(int lds_doubles, int nf);
+int solve_slack_doubles();
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
 // rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, hipStream_t s);
