@@ -66,32 +66,53 @@ def main():
 
     import uno_amd
     uno_amd.load_library()
-    dist_mode = world > 1 and args.mode == "dist"
-    if dist_mode:  # one system of dimension world * n, the same on every rank
-        seed = uno_amd.SEEDS["C3"]
-        n_total = args.n * world
-    else:          # independent system per rank
-        seed = uno_amd.SEEDS["C3"] + rank
-        n_total = args.n
-    n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(n_total, seed)
-    kkt = uno_amd.HipKKT(local)
-    if dist_mode:
-        from uno_amd.replicas import share_bytes
-        uid = share_bytes(uno_amd.rccl_unique_id() if rank == 0 else None, world)
-        kkt.attach_rccl(uid, rank, world)
-    if args.leaf:
-        kkt.set_option("leaf_size", args.leaf)
-    if args.block:
-        kkt.set_option("max_block", args.block)
-    kkt.set_option("dataflow_solve", args.dataflow)
-    t0 = time.perf_counter()
-    kkt.analyze(n, rows, cols)
-    t_analysis = time.perf_counter() - t0
+    def build(dist_mode):
+        if dist_mode:  # one system of dimension world * n, the same on every rank
+            seed, n_total = uno_amd.SEEDS["C3"], args.n * world
+        else:          # independent system per rank
+            seed, n_total = uno_amd.SEEDS["C3"] + rank, args.n
+        n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(n_total, seed)
+        kkt = uno_amd.HipKKT(local)
+        if dist_mode:
+            from uno_amd.replicas import share_bytes
+            uid = share_bytes(uno_amd.rccl_unique_id() if rank == 0 else None, world)
+            kkt.attach_rccl(uid, rank, world)
+        if args.leaf:
+            kkt.set_option("leaf_size", args.leaf)
+        if args.block:
+            kkt.set_option("max_block", args.block)
+        kkt.set_option("dataflow_solve", args.dataflow)
+        t0 = time.perf_counter()
+        kkt.analyze(n, rows, cols)
+        t_analysis = time.perf_counter() - t0
+        vals_d = torch.from_numpy(vals).to(dev)
+        rhs_d = torch.from_numpy(rhs).to(dev)
+        x_d = torch.empty_like(rhs_d)
+        torch.cuda.synchronize()
+        return n_total, (n, nv, m, rows, cols, vals, rhs), kkt, t_analysis, vals_d, rhs_d, x_d
 
-    vals_d = torch.from_numpy(vals).to(dev)
-    rhs_d = torch.from_numpy(rhs).to(dev)
-    x_d = torch.empty_like(rhs_d)
-    torch.cuda.synchronize()
+    dist_mode = world > 1 and args.mode == "dist"
+    dist_fallback = None
+    if dist_mode:
+        # the partitioned path is checked once before timing; a rank that fails (RCCL or device error)
+        # makes every rank fall back to independent replicas, reported in the JSON line
+        ok, err = 1, ""
+        try:
+            n_total, gen, kkt, t_analysis, vals_d, rhs_d, x_d = build(True)
+            kkt.factorize(device_ptr=vals_d.data_ptr())
+            kkt.inertia()
+            kkt.solve_device(rhs_d.data_ptr(), x_d.data_ptr())
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 -- reported, then the replicas mode runs
+            ok, err = 0, repr(e)[:300]
+        flag = torch.tensor([ok], dtype=torch.int32, device=dev)
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if int(flag.item()) == 0:
+            dist_fallback = err or "another rank failed"
+            dist_mode = False
+    if not dist_mode:
+        n_total, gen, kkt, t_analysis, vals_d, rhs_d, x_d = build(False)
+    n, nv, m, rows, cols, vals, rhs = gen
 
     def step():
         kkt.factorize(device_ptr=vals_d.data_ptr())
@@ -237,7 +258,7 @@ def main():
                    "parallelism": (f"subtree-partitioned x{world} (RCCL root exchange to rank 0)" if dist_mode
                                    else f"replicas x{world} (independent KKT per GPU)"),
                    "value_unit_note": "n=1e6-equivalent factor+solves per second of the whole job",
-                   "dist": dinfo},
+                   "dist": dinfo, "dist_fallback": dist_fallback},
         "roofline": roof,
         "cpu_baseline": cpu,
     }

@@ -144,6 +144,7 @@ struct uno_kkt {
     int df_enabled = 1;
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
     int df_win = 0, df_win_opt = 0; // LDS panel window of the dataflow solve (option solve_window, 0 = auto)
+    int df_piv_off = 0;
     uint32_t df_epoch = 0;
     bool df_rx_valid = false;      // rxpos matches the last factorization's pivoting
     bool df_check = false;         // a dataflow solve's abort flag copy is pending
@@ -257,6 +258,7 @@ DfArgs dataflow_args(uno_kkt_t h) {
     D.ch_cvx_off = h->df_ch_cvx_off.p; D.xs = h->df_xs.p; D.xs_off = h->df_xs_off.p; D.rxpos = h->df_rxpos.p;
     D.abort_flag = h->df_abort.p;
     D.win = h->df_win;
+    D.piv_off = h->df_piv_off;
     D.stamps = h->want_solve_stamps ? h->df_stamps.p : nullptr;
     return D;
 }
@@ -753,12 +755,13 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     // panel window: sized so that 16 one-wave blocks (4 per SIMD, the register limit of the dataflow
     // kernels) fit the 160 KB LDS of a CU; larger panels are processed in column windows
     const int rows_lds = ((mmax + 1) & ~1) + (mmax + 1) / 2;
-    int win = h->df_win_opt > 0 ? h->df_win_opt : (160 * 1024 / 16 - 16) / 8 - solve_slack_doubles() - rows_lds;
+    int win = h->df_win_opt > 0 ? h->df_win_opt : (160 * 1024 / 16 - 16) / 8 - solve_slack_doubles() - rows_lds - 32;
     win = std::max(win, mmax + 1) & ~1;
     win = std::min(win, (max_sz + 1) & ~1);
     win = std::max(win, 2);
     h->df_win = win;
-    const int lds = win + rows_lds;
+    h->df_piv_off = win + rows_lds;
+    const int lds = win + rows_lds + 32;  // + 64 pivot-kind words
     std::vector<int64_t> cvx(S.nf), xs(S.nf), chx(S.child.size());
     int64_t tc = 0, tx = 0;
     for (int64_t f = 0; f < S.nf; ++f) {

@@ -1834,7 +1834,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         // next position (clamped: the last front re-prefetches itself, branch-free loop-carried loads)
         const int tn = min(t + (int)gridDim.x, D.nf - 1);
         const int dn = df_desc_load(D, tn);  // next record: extracted after the children's loads
-        const int m = q.r.m, p = q.r.p, f = q.r.f, par = q.r.par, mypiv = q.mypiv;
+        const int m = q.r.m, p = q.r.p, f = q.r.f, par = q.r.par;
         const int64_t xoff = q.r.xoff, woff = q.r.woff;
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f : nullptr;
         if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
@@ -1843,6 +1843,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         int32_t* fpl = (int32_t*)(y + ((m + 1) & ~1));  // this front's rows were permuted by pivoting
         const int k1 = q.kw;
         const int64_t Lo = q.r.Lo;
+        // pivot kinds through LDS: a register copy of q.mypiv (reloaded by df_issue below) would make the
+        // loop back-edge wait for the next front's prefetch
+        int32_t* ipl = (int32_t*)(smem_s + D.piv_off);
+        ipl[lane] = q.mypiv;
         if (lane < m) { y[lane] = q.e0; fpl[lane] = q.fp0; }
         if (lane + 64 < m) { y[lane + 64] = 0.0; fpl[lane + 64] = q.fp1; }
         const uint32_t target = D.epoch * (uint32_t)(q.r.c1 - q.r.c0);
@@ -1859,6 +1863,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         q.r = df_record(dn);
         df_issue<true>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+        const int mypiv = ipl[lane];
         fwd_compute_win(A.L, Lo, m, p, P, D.win, k1, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         pend = par;
@@ -1884,7 +1889,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     for (; t < D.nf; t += gridDim.x) {
         const int tn = min(t + (int)gridDim.x, D.nf - 1);
         const int dn = df_desc_load(D, D.nf - 1 - tn);
-        const int m = q.r.m, p = q.r.p, f = q.r.f, mypiv = q.mypiv;
+        const int m = q.r.m, p = q.r.p, f = q.r.f;
         const int64_t woff = q.r.woff;
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f + 4 : nullptr;
         if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
@@ -1898,6 +1903,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
             signal();
             df_wait(D.done + q.r.par, D.epoch, D.abort_flag);
         }
+        int32_t* ipl = (int32_t*)(smem_s + D.piv_off);  // pivot kinds through LDS (see k_solve_fwd_df)
+        ipl[lane] = q.mypiv;
         if (lane < m) x[lane] = lane < p ? q.e0 : ld_sc1(D.xs + q.a0);
         if (lane + 64 < m) x[lane + 64] = ld_sc1(D.xs + q.a1);
         df_stage_window(A, q, P);
@@ -1907,6 +1914,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         q.r = df_record(dn);
         df_issue<false>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+        const int mypiv = ipl[lane];
         const double xj = bwd_compute_win(A.L, Lo, m, p, P, D.win, c0, x, mypiv);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (lane < p) st_sc1(D.xs + woff + lane, xj);

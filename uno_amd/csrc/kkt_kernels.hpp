@@ -93,6 +93,7 @@ struct DfArgs {
     const int32_t* rxpos;       // per front row (layout of frow): xs index of the rows >= p
     uint32_t* abort_flag;       // set when a wait exceeded its limit (result invalid, host falls back)
     int32_t win;                // LDS panel window (doubles, even, >= the longest column); rows follow it
+    int32_t piv_off;            // LDS offset (doubles) of the 64 pivot-kind words, after the rows
     unsigned long long* stamps; // diagnostics (nullptr in normal runs): per front and direction 4 s_memrealtime
                                 // words {start, dependency satisfied, values staged, published}
 };
