@@ -83,15 +83,18 @@ __device__ __forceinline__ void row_scan(int32_t i, int lane, const ScanArgs& A,
 
 template <int MODE>
 __global__ void k_rowscan(ScanArgs A) {
-    const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / 16;
-    const int lane = threadIdx.x & 15;
+    // max scans (MODE 0/1) are order-free, so they use 8 lanes per row (more rows in flight); the sum
+    // scan keeps 16 lanes so its summation order, and hence ||A_pre||_inf, is unchanged
+    constexpr int LPR = MODE == 2 ? 16 : 8;
+    const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int lane = threadIdx.x & (LPR - 1);
     if (g >= A.n) return;
     const int32_t i = A.list ? A.list[g] : (int32_t)g;
     if ((A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > kLongRow) {
         if (lane == 0) A.out[A.perm[i]] = 0.0;  // combined by k_rowscan_long
         return;
     }
-    row_scan<16, MODE>(i, lane, A, nullptr);
+    row_scan<LPR, MODE>(i, lane, A, nullptr);
 }
 
 // Long (dense) rows: each row is cut into chunks of kLongChunk entries, one workgroup per chunk,
@@ -1971,7 +1974,7 @@ hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32
 
 hipError_t launch_rowscan(const ScanArgs& A, int mode, hipStream_t s) {
     if (A.n > 0) {
-        const int64_t threads = A.n * 16;
+        const int64_t threads = A.n * (mode == 2 ? 16 : 8);  // lanes per row, as in k_rowscan
         const dim3 g((unsigned)((threads + 255) / 256));
         if (mode == 0) hipLaunchKernelGGL(k_rowscan<0>, g, dim3(256), 0, s, A);
         else if (mode == 1) hipLaunchKernelGGL(k_rowscan<1>, g, dim3(256), 0, s, A);
