@@ -7,8 +7,9 @@ Uno's ipopt-preset layout, uno_amd/csrc/arrowband.c).  A step is one numerical L
 side are already resident in HBM when the timed region starts.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N), default
---mode dist: ONE arrowband KKT of dimension N x 1e6 (weak scaling: 1e6 rows per
-GPU) is factored and solved across the N GPUs -- independent elimination subtrees per rank, the
+--mode dist: ONE arrowband KKT of the C5 family (seed 0x5EED0005) of dimension
+N x 5e5 (weak scaling: 5e5 rows per GPU, so N = 8 is exactly BASELINE.json configs[4], n = 4e6,
+nnz = 8e7) is factored and solved across the N GPUs -- independent elimination subtrees per rank, the
 subtree roots' contribution blocks / update vectors sent to rank 0 over RCCL (xGMI) for the top of
 the assembly tree, the top rows of the solution broadcast back, inertia all-reduced, the solution
 gathered on rank 0.  value = (N x 1e6 / 1e6) factor+solves per second, i.e. n=1e6-equivalent
@@ -39,7 +40,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=1_000_000, help="KKT dimension per GPU (C3 = 1e6)")
+    ap.add_argument("--n", type=int, default=0,
+                    help="KKT dimension per GPU (default: 1e6 = C3 on one GPU / in replicas; 5e5 per GPU in dist mode, "
+                         "C5 = 4e6 at 8 GPUs)")
     ap.add_argument("--mode", choices=["dist", "replicas"], default="dist",
                     help="N>1: one system partitioned over the GPUs (dist) or one system per GPU (replicas)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -67,10 +70,10 @@ def main():
     import uno_amd
     uno_amd.load_library()
     def build(dist_mode):
-        if dist_mode:  # one system of dimension world * n, the same on every rank
-            seed, n_total = uno_amd.SEEDS["C3"], args.n * world
+        if dist_mode:  # one C5-family system of dimension world * n, the same on every rank
+            seed, n_total = uno_amd.SEEDS["C5"], (args.n or 500_000) * world
         else:          # independent system per rank
-            seed, n_total = uno_amd.SEEDS["C3"] + rank, args.n
+            seed, n_total = uno_amd.SEEDS["C3"] + rank, args.n or 1_000_000
         n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(n_total, seed)
         kkt = uno_amd.HipKKT(local)
         if dist_mode:
@@ -122,6 +125,22 @@ def main():
 
     from uno_amd.replicas import aggregate, timed_steps
     elapsed, inertia = timed_steps(step, args.steps, args.warmup, torch.cuda.synchronize, world, dev)
+    # also the median of >= 20 individually synchronised steps (reported beside the
+    # contract's K-step wall time)
+    per_step = []
+    for _ in range(max(20, args.steps) if not args.profile_only else 0):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        step()
+        torch.cuda.synchronize()
+        per_step.append(time.perf_counter() - t1)
+    if world > 1 and per_step:
+        tt = torch.tensor(per_step, dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        per_step = tt.cpu().tolist()
+    median_ms = round(1e3 * float(np.median(per_step)), 4) if per_step else None
 
     # parity sanity on the measured system: relative residual of the last solve (rank 0 holds the
     # complete solution in dist mode)
@@ -225,13 +244,17 @@ def main():
         while reps < 3 and t_cpu < 20.0:
             t1 = time.perf_counter()
             o.factorize(cv)
-            o.inertia()
+            o_inertia = o.inertia()
             o.solve(cb)
             t_cpu += time.perf_counter() - t1
             reps += 1
+        # parity on the measured system: the GPU inertia of the timed steps is the oracle's
+        if cn == n:
+            assert tuple(o_inertia) == tuple(inertia), f"GPU inertia {inertia} != oracle {o_inertia}"
         cpu = {"value": round(reps / t_cpu, 5), "unit": "factor+solve/s", "cores": 1, "kind": "port",
                "sample": f"oracle/kkt_oracle.c (MUMPS sym=2 restatement; MUMPS unavailable) on arrowband "
-                         f"n={cn} nnz={len(cv)}, {reps} factor+inertia+solve reps, {t_cpu:.2f} s, 1 thread"}
+                         f"n={cn} nnz={len(cv)}, {reps} factor+inertia+solve reps, {t_cpu:.2f} s, 1 thread",
+               "inertia": list(o_inertia), "inertia_checked_against_gpu": cn == n}
 
     out = {
         "metric": "KKT factor+solve/sec & HBM GB/s, n=1e6 nnz=2e7 ipopt preset, 1/2/4/8 GPU",
@@ -241,13 +264,15 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_per_step, 4),
+        "ms_per_step_median": median_ms,
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": ("synthetic (arrowband KKT generator, SURVEY 8(d), seed 0x5EED0003, one system over all ranks)"
+        "data": ("synthetic (arrowband KKT generator, SURVEY 8(d), C5 family seed 0x5EED0005, one system over all ranks)"
                  if dist_mode else "synthetic (arrowband KKT generator, SURVEY 8(d), seed 0x5EED0003+rank)"),
-        "config": {"workload": "C3 arrowband KKT, ipopt-preset COO layout, factor+inertia+solve",
+        "config": {"workload": ("C5-family arrowband KKT (n = %d over %d GPUs), ipopt-preset COO layout, factor+inertia+solve"
+                                % (n_total, world)) if dist_mode else "C3 arrowband KKT, ipopt-preset COO layout, factor+inertia+solve",
                    "n": n, "nv": nv, "m": m, "nnz": int(len(vals)), "nnz_unique": st["nnz_unique"],
                    "nnz_L": st["nnz_L"], "fronts": st["n_fronts"], "levels": st["n_levels"],
                    "max_front": st["max_front"], "ordering": "nested dissection (BFS level sets), 6 dense nodes last",

@@ -158,6 +158,23 @@ int main(int argc, char* argv[]) {
          ps += v; pq += v * v; pm = std::max(pm, std::fabs(v));
       }
       std::printf("], \"primals_summary\": [%.17g, %.17g, %.17g", ps, pq, pm);
+      // dual side (north_star: primal/dual residuals): multipliers of the constraints and of the bounds,
+      // and the reference's own residual measures of the final iterate (Iterate.hpp:43-46, DualResiduals.hpp)
+      const auto print_vector = [](const char* name, const Vector<double>& v, size_t count, bool full) {
+         std::printf("], \"%s\": [", name);
+         if (full) {
+            for (size_t i = 0; i < count; ++i) std::printf("%s%.17g", i ? ", " : "", v[i]);
+         }
+         double s = 0., q = 0., m = 0.;
+         for (size_t i = 0; i < count; ++i) { s += v[i]; q += v[i] * v[i]; m = std::max(m, std::fabs(v[i])); }
+         std::printf("], \"%s_summary\": [%.17g, %.17g, %.17g", name, s, q, m);
+      };
+      const bool full = result.number_variables <= 64 && result.number_constraints <= 64;
+      print_vector("constraint_multipliers", result.solution.multipliers.constraints, result.number_constraints, full);
+      print_vector("lower_bound_multipliers", result.solution.multipliers.lower_bounds, result.number_variables, full);
+      print_vector("upper_bound_multipliers", result.solution.multipliers.upper_bounds, result.number_variables, full);
+      std::printf("], \"residuals\": [%.17g, %.17g, %.17g", result.solution.primal_feasibility,
+         result.solution.residuals.stationarity, result.solution.residuals.complementarity);
       size_t nf = 0, ns = 0;
       for (const auto& e: kkt_trace::events()) {
          (e.kind == 'F' ? nf : ns)++;

@@ -11,6 +11,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: full-size (C3) parity properties")
+    config.addinivalue_line("markers", "needs_driver: runs the reference Uno core through oracle/_ref/uno_kkt_driver")
 
 
 @pytest.fixture(scope="session", autouse=True)

@@ -14,9 +14,14 @@ oracle/_ref/uno_kkt_driver arrowband:10000 linear_solver=ORACLE logger=SILENT | 
 # the inequality-constrained variant (-1 <= A x - b <= 1: slacks in the ipopt preset), SURVEY 8(f) item 4
 oracle/_ref/uno_kkt_driver arrowband_ineq:10000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
   > tests/golden/arrowband_ineq10000_uno_oracle.json
-# n = 1e5 (4.5 min on one core; compared by the GPU test only)
+# n = 1e5 (4.5 min on one core; compared by the GPU test only) and its inequality-constrained variant
+# (configs[3] fallback at the stated size); both in parallel
 oracle/_ref/uno_kkt_driver arrowband:100000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
-  > tests/golden/arrowband100000_uno_oracle.json
+  > tests/golden/arrowband100000_uno_oracle.json &
+oracle/_ref/uno_kkt_driver arrowband_ineq:100000 linear_solver=ORACLE logger=SILENT | grep '^{' | tail -n 1 \
+  > tests/golden/arrowband_ineq100000_uno_oracle.json &
+wait
+[ "${1:-}" = "--no-convexify" ] && exit 0
 # byrd-preset Hessian convexification (PrimalRegularization::regularize_hessian on the l1-relaxed problem's
 # Hessian at a fixed sequence of points; driver mode convexify:<model>)
 python3 - <<'PY'

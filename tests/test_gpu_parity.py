@@ -230,3 +230,33 @@ def test_dataflow_panel_windows(uno_amd, window):
     for rep in range(2):
         np.testing.assert_array_equal(gd.solve(b * (rep + 1)), gl.solve(b * (rep + 1)))
     assert gd.stats()["solve_aborts"] == 0
+
+
+@pytest.mark.slow
+def test_c3_full_size(uno_amd):
+    """The headline configuration itself (BASELINE.json configs[2], SURVEY.md 8(d) C3: arrowband KKT
+    n = 1e6, nnz = 2e7, seed 0x5EED0003): inertia identical to the oracle's, solution within 1e-6 of the
+    oracle's (different orderings: ND vs RCM), relative residual <= 1e-10; then one inertia-correction
+    retry (delta_w / delta_c edited on the device, PrimalDualRegularization.hpp:178-179) with the same
+    checks, and a second solve that must be bit-identical to the first (deterministic kernels)."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(1_000_000, SEEDS["C3"])
+    g, o = both(n, r, c, v)
+    assert g.inertia() == o.inertia()
+    xg = g.solve(b)
+    assert rel_residual(n, r, c, v, xg, b) < RES_TOL
+    np.testing.assert_allclose(xg, o.solve(b), rtol=1e-6, atol=1e-9 * np.abs(xg).max())
+    np.testing.assert_array_equal(g.solve(b), xg)
+    g.fill_values(0, nv, 1e-4)
+    g.fill_values(nv, m, -1e-8)
+    g.factorize()
+    v2 = v.copy()
+    v2[:nv] = 1e-4
+    v2[nv:n] = -1e-8
+    o.factorize(v2)
+    assert g.inertia() == o.inertia()
+    xg = g.solve(b)
+    assert rel_residual(n, r, c, v2, xg, b) < RES_TOL
+    np.testing.assert_allclose(xg, o.solve(b), rtol=1e-6, atol=1e-9 * np.abs(xg).max())
+    st = g.stats()
+    assert st["solve_aborts"] == 0 and st["factor_df_aborts"] == 0

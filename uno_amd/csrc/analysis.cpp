@@ -324,6 +324,7 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
         int64_t p = bfirst[b + 1] - bfirst[b];
         int64_t m = p + (soff[b + 1] - soff[b]);
         if (m > 65535) return "front order exceeds 65535";
+        if (p > 32767) return "supernode wider than 32767 columns";
         S.f_m[b] = (int32_t)m;
         S.f_p[b] = (int32_t)p;
         S.max_m = std::max<int64_t>(S.max_m, m);
@@ -440,7 +441,10 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
             if (lr < 0) return "internal: entry row missing from its front";
             S.ent_r[s] = S.perm[hi];
             S.ent_c[s] = S.perm[lo];
-            S.ent_lpos[s] = ((uint32_t)lr << 16) | (uint32_t)lc;
+            // bit 15: the column's original id is the larger one, so the oracle's scaled value
+            // (s[larger] * v) * s[smaller] is (s_col * v) * s_row (kkt_kernels.hip assemble_front)
+            const uint32_t flip = S.perm[lo] > S.perm[hi] ? 0x8000u : 0u;
+            S.ent_lpos[s] = ((uint32_t)lr << 16) | flip | (uint32_t)lc;
             if (!S.identity_dups) S.dup_ptr[s + 1] = P.udp[u + 1] - P.udp[u];
         }
         if (S.identity_dups) {

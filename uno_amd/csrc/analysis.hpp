@@ -43,7 +43,8 @@ struct Symbolic {
     bool identity_dups = false;        // every unique entry has exactly one COO position
     std::vector<int32_t> dup_ptr, dup_pos;
     std::vector<int32_t> ent_r, ent_c; // original ids, ent_r is the later-eliminated one
-    std::vector<uint32_t> ent_lpos;    // (local row << 16) | local col inside the owning front
+    std::vector<uint32_t> ent_lpos;    // (local row << 16) | flip << 15 | local col inside the owning front
+                                       // (flip: the column has the larger original id)
     // row-wise access to the packed slots (new numbering) for atomic-free equilibration:
     // column part of row i = slots [cptr[i], cptr[i+1]) (entries (r, i), r >= i, contiguous),
     // row part = rslot[rptr[i] .. rptr[i+1]) (entries (i, c), c < i)

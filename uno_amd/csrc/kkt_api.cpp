@@ -83,7 +83,9 @@ struct DistState {
     DBuf<int32_t> top_orig;                                // rows eliminated in top fronts
     int64_t n_top_rows = 0;
     DBuf<int32_t> chunk_row, pslot, ppartner;              // partial scans of the top rows
-    DBuf<int64_t> chunk_begin;
+    DBuf<int64_t> chunk_begin, row_chunk;
+    DBuf<double> chunk_part, own_long_part;               // chunk results (combined in chunk order)
+    int64_t own_long_chunks = 0;
     int64_t nchunks = 0;
     DBuf<double> outT, tbuf, xbuf;
     DBuf<unsigned long long> tmp;
@@ -113,7 +115,8 @@ struct uno_kkt {
     int64_t exact_redos = 0;
     AnalysisOptions aopt;
     double u = 0.01, null_fac = 1e-5;
-    int scale_iters = 1;
+    // ICNTL(8)=8 restated as 3 symmetric infinity-norm sweeps, the oracle's value (oracle/kkt_oracle.c)
+    int scale_iters = 3;
     int timing = 0;
     Pattern P;
     Symbolic S;
@@ -135,7 +138,8 @@ struct uno_kkt {
     int want_stamps = 0;
     DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed;
     int32_t n_long = 0;
-    int64_t max_long = 0;
+    int64_t max_long = 0, long_chunks = 0;
+    DBuf<double> long_part;  // chunk results of the long-row scans
     unsigned long long* h_counters = nullptr;
     Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
     Plan dff_plan; // factor launches of the own fronts outside the dataflow launch (dff active)
@@ -147,7 +151,6 @@ struct uno_kkt {
     int df_piv_off = 0;
     uint32_t df_epoch = 0;
     bool df_rx_valid = false;      // rxpos matches the last factorization's pivoting
-    bool df_check = false;         // a dataflow solve's abort flag copy is pending
     int64_t df_aborts = 0;
     DBuf<int32_t> df_order, df_desc, df_xpos, df_rxpos;
     DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
@@ -172,6 +175,8 @@ struct uno_kkt {
     DBuf<int32_t> jv_ent, j_con;
     DBuf<unsigned long long> alpha;
     DBuf<double> symv_tmp, symv_part, dot_d;
+    DBuf<int64_t> edit_pos;               // uno_kkt_set_values staging
+    DBuf<double> edit_val;
     bool packed_valid = false;            // uval holds the current values (symv reuses the factor's pack)
     ukkt::Transport* comm = nullptr;
     int rank = 0, world = 1;
@@ -264,20 +269,17 @@ DfArgs dataflow_args(uno_kkt_t h) {
 }
 
 // After the stream has drained: a dataflow solve whose waits hit their limit produced no valid
-// solution; the counters are cleared and the level schedule is used from then on.
-int check_dataflow(uno_kkt_t h) {
-    h->df_check = false;
+// solution (k_xs_out then leaves x untouched); the flag is cleared and the level schedule is used from
+// then on.  Returns true if the solve aborted.
+bool dataflow_aborted(uno_kkt_t h) {
     uint32_t ab = 0;
     memcpy(&ab, h->h_counters + 10, sizeof(ab));
-    if (ab == 0) return UNO_KKT_OK;
+    if (ab == 0) return false;
     h->df_aborts++;
     h->df_enabled = 0;
     h->df_grid = 0;
     memset(h->h_counters + 10, 0, 8);
-    HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), h->stream));
-    HIPCHK(h, hipStreamSynchronize(h->stream));
-    return set_err(h, UNO_KKT_ERR_HIP, "dataflow solve aborted (dependency wait limit): the last device solution is "
-                                       "invalid; level-scheduled solves from now on");
+    return true;
 }
 
 // Launch plan of the fronts selected by `take`: per level, fronts sorted by order (descending) cut
@@ -427,7 +429,7 @@ int setup_distribution(uno_kkt_t h) {
     HIPCHK(h, D.top_orig.upload(top_orig, s));
     // partial scans of the top rows: this rank's slots of each top row, in chunks
     std::vector<int32_t> crow, pslot, ppart;
-    std::vector<int64_t> cbeg;
+    std::vector<int64_t> cbeg, rchunk;
     auto slot_front = [&](int64_t q) {
         return (int32_t)(std::upper_bound(S.f_ent_off.begin(), S.f_ent_off.end(), q) - S.f_ent_off.begin() - 1);
     };
@@ -440,10 +442,16 @@ int setup_distribution(uno_kkt_t h) {
             const int32_t q = S.rslot[t2];
             if (mine(slot_front(q))) { pslot.push_back(q); ppart.push_back(S.ent_c[q] == o ? S.ent_r[q] : S.ent_c[q]); }
         }
+        rchunk.push_back((int64_t)crow.size());
         for (size_t b = start; b < pslot.size(); b += kLongChunk) { crow.push_back((int32_t)t); cbeg.push_back((int64_t)b); }
     }
     cbeg.push_back((int64_t)pslot.size());
+    rchunk.push_back((int64_t)crow.size());
     D.nchunks = (int64_t)crow.size();
+    HIPCHK(h, D.row_chunk.upload(rchunk, s));
+    HIPCHK(h, D.chunk_part.alloc(std::max<int64_t>(D.nchunks, 1)));
+    D.own_long_chunks = (D.max_own_long + kLongChunk - 1) / kLongChunk;
+    HIPCHK(h, D.own_long_part.alloc(std::max<int64_t>((int64_t)D.n_own_long * D.own_long_chunks, 1)));
     HIPCHK(h, D.chunk_row.upload(crow, s));
     HIPCHK(h, D.chunk_begin.upload(cbeg, s));
     HIPCHK(h, D.pslot.upload(pslot, s));
@@ -500,14 +508,16 @@ int dist_scale(uno_kkt_t h, ScanArgs SA) {
     SA.long_rows = D.own_long.p;
     SA.n_long = D.n_own_long;
     SA.max_long = D.max_own_long;
+    SA.long_chunks = D.own_long_chunks;
+    SA.part = D.own_long_part.p;
     PartArgs PA;
     PA.nchunks = D.nchunks; PA.chunk_row = D.chunk_row.p; PA.chunk_begin = D.chunk_begin.p; PA.pslot = D.pslot.p;
     PA.ppartner = D.ppartner.p; PA.trow_orig = D.top_orig.p; PA.uval = h->uval.p; PA.scale = h->scale.p;
     PA.outT = D.outT.p;
+    PA.nrows = D.n_top_rows; PA.row_chunk = D.row_chunk.p; PA.part = D.chunk_part.p;
     const int64_t nt = D.n_top_rows;
     auto top_pass = [&](int mode, double* out, RedOp op) -> int {
         if (nt == 0) return UNO_KKT_OK;
-        HIPCHK(h, hipMemsetAsync(D.outT.p, 0, sizeof(double) * nt, s));
         HIPCHK(h, launch_rowscan_part(PA, mode, s));
         HIPCHK(h, h->comm->allreduce(D.outT.p, (size_t)nt, op, s));
         HIPCHK(h, launch_scatter(D.outT.p, D.top_orig.p, out, nt, s));
@@ -880,6 +890,8 @@ int upload_structure(uno_kkt_t h) {
         }
         h->n_long = (int32_t)lr.size();
         HIPCHK(h, h->long_rows.upload(lr, s));
+        h->long_chunks = (h->max_long + kLongChunk - 1) / kLongChunk;
+        HIPCHK(h, h->long_part.alloc(std::max<int64_t>((int64_t)h->n_long * h->long_chunks, 1)));
     }
     if (h->delayed.n != (size_t)std::max<int64_t>(n, 1)) HIPCHK(h, h->delayed.alloc(std::max<int64_t>(n, 1)));
     if (h->uval.n != (size_t)S.nu) HIPCHK(h, h->uval.alloc(S.nu));
@@ -959,7 +971,7 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.n = S.n; SA.list = nullptr; SA.perm = h->perm_d.p; SA.cptr = h->cptr.p; SA.rptr = h->rptr.p;
         SA.rslot = h->rslot.p; SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p;
         SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p;
-        SA.n_long = h->n_long; SA.max_long = h->max_long;
+        SA.n_long = h->n_long; SA.max_long = h->max_long; SA.long_chunks = h->long_chunks; SA.part = h->long_part.p;
         if (h->world == 1 && h->overlap_norm && !h->exact_next) {
             HIPCHK(h, launch_scale_sweeps(SA, h->scale_iters, h->rmax.p, s));
             HIPCHK(h, hipEventRecord(h->ev_scale, s));
@@ -1178,14 +1190,23 @@ int uno_kkt_set_values(uno_kkt_t h, const int64_t* positions, const double* v, i
     if (!h->analyzed || !h->values_ptr) return set_err(h, UNO_KKT_ERR_STATE, "set_values before a factorization");
     if (count < 0 || (count > 0 && (!positions || !v))) return set_err(h, UNO_KKT_ERR_ARG, "bad arguments");
     HIPCHK(h, hipSetDevice(h->device));
-    h->packed_valid = false;
-    // small host-driven edit: positions are few (regularization diagonal), copy one by one in batches
-    for (int64_t i = 0; i < count; ++i) {
+    for (int64_t i = 0; i < count; ++i)
         if (positions[i] < 0 || positions[i] >= h->S.nnz) return set_err(h, UNO_KKT_ERR_ARG, "position out of range");
-        HIPCHK(h, hipMemcpyAsync(const_cast<double*>(h->values_ptr) + positions[i], v + i, sizeof(double),
-                                 hipMemcpyHostToDevice, h->stream));
+    // the values of a queued factorization are final only once it has been checked (its redos re-pack
+    // from the same buffer): finish it before editing
+    if (h->factor_enqueued) {
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
     }
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    h->packed_valid = false;
+    if (count == 0) return UNO_KKT_OK;
+    // one H2D copy of (positions, values), one scatter kernel
+    HIPCHK(h, h->edit_pos.alloc(count));
+    HIPCHK(h, h->edit_val.alloc(count));
+    HIPCHK(h, hipMemcpyAsync(h->edit_pos.p, positions, sizeof(int64_t) * count, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->edit_val.p, v, sizeof(double) * count, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, launch_scatter64(h->edit_val.p, h->edit_pos.p, const_cast<double*>(h->values_ptr), count, h->stream));
+    HIPCHK(h, hipStreamSynchronize(h->stream));  // the host arrays may be reused on return
     return UNO_KKT_OK;
 }
 
@@ -1203,6 +1224,10 @@ int uno_kkt_fill_values(uno_kkt_t h, int64_t first, int64_t count, double value)
     if (first < 0 || count < 0 || first + count > h->S.nnz) return set_err(h, UNO_KKT_ERR_ARG, "range out of bounds");
     if (count == 0) return UNO_KKT_OK;
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->factor_enqueued) {  // see uno_kkt_set_values
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
+    }
     h->packed_valid = false;
     int grid = (int)std::min<int64_t>((count + 255) / 256, 4096);
     hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, h->stream, const_cast<double*>(h->values_ptr) + first, count, value);
@@ -1216,8 +1241,10 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     HIPCHK(h, hipSetDevice(h->device));
     Symbolic& S = h->S;
     if (h->factor_enqueued) {  // previous factorization never queried: drain it first
+        // a device / runtime failure is reported; a pivoting failure (ERR_PIVOT) only concerned the
+        // drained values, which this factorization replaces
         int rc = finish_factorization(h);
-        (void)rc;
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
     }
     h->factored = false;
     if (values == nullptr) {
@@ -1249,11 +1276,6 @@ int uno_kkt_inertia(uno_kkt_t h, int64_t* positive, int64_t* negative, int64_t* 
 
 int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     if (!h || !rhs || !x) return UNO_KKT_ERR_ARG;
-    if (h->df_check) {  // the previous (device-pointer) dataflow solve: aborted waits invalidate it
-        HIPCHK(h, hipStreamSynchronize(h->stream));
-        int rc = check_dataflow(h);
-        if (rc != UNO_KKT_OK) return rc;
-    }
     if (!h->analyzed || (!h->factored && !h->factor_enqueued))
         return set_err(h, UNO_KKT_ERR_STATE, "solve before factorize");
     HIPCHK(h, hipSetDevice(h->device));
@@ -1308,8 +1330,6 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
             TimerScope t(h, KC_SOLVE_BWD);
             HIPCHK(h, launch_solve_df(A, D, h->df_grid, h->df_lds, false, s));
         }
-        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        h->df_check = true;
     }
     for (size_t q = 0; q < P0.sol.size() && !df; ++q) {
         TimerScope t(h, KC_SOLVE_FWD);
@@ -1343,7 +1363,7 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
     double* xd = on_device ? x : h->bvec.p;
     {
         TimerScope t(h, KC_RHS);
-        if (df) HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, xd, S.n, s));
+        if (df) HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, S.n, s));
         else HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
     }
     if (h->world > 1 && h->gather_solution) {
@@ -1361,21 +1381,31 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         if (h->rank == 0)
             HIPCHK(h, launch_scatter(D.xbuf.p, D.all_own_orig.p, xd, D.all_own_off[h->world], s));
     }
+    if (df) {
+        // a dataflow solve is checked in the same call: on an abort k_xs_out has left x (and so an aliased
+        // rhs) untouched, and the solve is redone with the level schedule
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        if (dataflow_aborted(h)) {
+            HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
+            if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: redone level by level\n");
+            return uno_kkt_solve(h, rhs, x, on_device);
+        }
+    }
     h->st.solves++;
     if (!on_device) {
         if (S.n > 0) HIPCHK(h, hipMemcpyAsync(x, xd, S.n * sizeof(double), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
-        if (df && check_dataflow(h) != UNO_KKT_OK) {
-            h->err.clear();
-            return uno_kkt_solve(h, rhs, x, on_device);  // level schedule (dataflow now disabled)
-        }
     }
     return UNO_KKT_OK;
 }
 
 int uno_kkt_stats(uno_kkt_t h, uno_kkt_stats_t* out) {
     if (!h || !out) return UNO_KKT_ERR_ARG;
-    if (h->factor_enqueued) finish_factorization(h);
+    if (h->factor_enqueued) {
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
+    }
     *out = h->st;
     out->fronts_merged = h->merges_total;
     out->solve_grid = (h->world == 1 && h->df_enabled) ? h->df_grid : 0;

@@ -47,6 +47,14 @@ __global__ void k_pack(const double* __restrict__ values, const int32_t* __restr
     }
 }
 
+// |s_a v s_b| evaluated as (s_a * v) * s_b with a the larger original index: the oracle's expression
+// (oracle/kkt_oracle.c, sv[u] = s[ur] * uval[u] * s[uc], ur > uc), so the scaling vectors and the scaled
+// entries are bit-identical to the oracle's whatever the row a scan visits the entry from
+__device__ __forceinline__ double scaled_abs(int32_t i, double si, int32_t j, double v, const double* __restrict__ scale) {
+    const double sj = scale[j];
+    return i > j ? fabs(si * v * sj) : fabs(sj * v * si);
+}
+
 // Row-wise scans of the packed matrix (new numbering), atomic-free:
 //   MODE 0: rmax_i = max_j |a_ij|               (first equilibration sweep, s = 1)
 //   MODE 1: rmax_i = max_j |s_i a_ij s_j|       (later sweeps)
@@ -58,12 +66,12 @@ __device__ __forceinline__ void row_scan(int32_t i, int lane, const ScanArgs& A,
     const double si = MODE > 0 ? A.scale[orig] : 1.0;
     double acc = 0.0;
     for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += LPR) {
-        double w = MODE == 0 ? fabs(A.uval[q]) : fabs(si * A.uval[q] * A.scale[A.ent_r[q]]);
+        double w = MODE == 0 ? fabs(A.uval[q]) : scaled_abs(orig, si, A.ent_r[q], A.uval[q], A.scale);
         acc = MODE == 2 ? acc + w : fmax(acc, w);
     }
     for (int32_t t = A.rptr[i] + lane; t < A.rptr[i + 1]; t += LPR) {
         const int32_t q = A.rslot[t];
-        double w = MODE == 0 ? fabs(A.uval[q]) : fabs(si * A.uval[q] * A.scale[A.ent_c[q]]);
+        double w = MODE == 0 ? fabs(A.uval[q]) : scaled_abs(orig, si, A.ent_c[q], A.uval[q], A.scale);
         acc = MODE == 2 ? acc + w : fmax(acc, w);
     }
     const int wl = LPR < 64 ? LPR : 64;
@@ -97,8 +105,9 @@ __global__ void k_rowscan(ScanArgs A) {
     row_scan<LPR, MODE>(i, lane, A, nullptr);
 }
 
-// Long (dense) rows: each row is cut into chunks of kLongChunk entries, one workgroup per chunk,
-// combined with one atomic per workgroup (a handful of rows, so contention is negligible).
+// Long (dense) rows: each row is cut into chunks of kLongChunk entries, one workgroup per chunk; the
+// chunk results go to A.part[row * A.long_chunks + chunk] and k_rowscan_long_fin combines them in chunk
+// order (no atomics: the row sums, hence ||A_pre||_inf, are the same in every run).
 template <int MODE>
 __global__ void k_rowscan_long(ScanArgs A) {
     __shared__ double red[kThreads / 64];
@@ -115,7 +124,7 @@ __global__ void k_rowscan_long(ScanArgs A) {
         int32_t q, partner;
         if (t < nc) { q = A.cptr[i] + (int32_t)t; partner = A.ent_r[q]; }
         else { q = A.rslot[A.rptr[i] + (int32_t)(t - nc)]; partner = A.ent_c[q]; }
-        double w = MODE == 0 ? fabs(A.uval[q]) : fabs(si * A.uval[q] * A.scale[partner]);
+        double w = MODE == 0 ? fabs(A.uval[q]) : scaled_abs(orig, si, partner, A.uval[q], A.scale);
         acc = MODE == 2 ? acc + w : fmax(acc, w);
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -126,14 +135,30 @@ __global__ void k_rowscan_long(ScanArgs A) {
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < kThreads / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
-        if (MODE == 2) atomicAdd(A.out + orig, acc);
-        else atomicMax((unsigned long long*)(A.out + orig), as_bits(acc));  // non-negative doubles
+        A.part[(int64_t)blockIdx.y * A.long_chunks + blockIdx.x] = acc;
     }
 }
 
+// one lane per long row: its chunk results in chunk order
+template <int MODE>
+__global__ void k_rowscan_long_fin(ScanArgs A) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n_long) return;
+    const int32_t i = A.long_rows[r];
+    const int64_t len = (A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]);
+    const int64_t nch = (len + kLongChunk - 1) / kLongChunk;
+    double acc = 0.0;
+    for (int64_t c = 0; c < nch; ++c) {
+        const double w = A.part[(int64_t)r * A.long_chunks + c];
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    A.out[A.perm[i]] = acc;
+}
+
 // Partial row scans of the separator ("top") rows on one rank of a distributed factorization: the
-// rank's own slots of each top row, cut into chunks (one workgroup each), combined per row with one
-// atomic per workgroup; the ranks' partials are then all-reduced (max / sum) over the top rows.
+// rank's own slots of each top row, cut into chunks (one workgroup each, results in A.part), combined
+// per row in chunk order by k_rowscan_part_fin; the ranks' partials are then all-reduced (max / sum)
+// over the top rows.
 template <int MODE>
 __global__ void k_rowscan_part(PartArgs A) {
     __shared__ double red[kThreads / 64];
@@ -144,7 +169,7 @@ __global__ void k_rowscan_part(PartArgs A) {
     double acc = 0.0;
     for (int64_t q = A.chunk_begin[c] + threadIdx.x; q < A.chunk_begin[c + 1]; q += kThreads) {
         const int32_t slot = A.pslot[q];
-        const double w = MODE == 0 ? fabs(A.uval[slot]) : fabs(si * A.uval[slot] * A.scale[A.ppartner[q]]);
+        const double w = MODE == 0 ? fabs(A.uval[slot]) : scaled_abs(orig, si, A.ppartner[q], A.uval[slot], A.scale);
         acc = MODE == 2 ? acc + w : fmax(acc, w);
     }
     for (int off = 32; off > 0; off >>= 1) {
@@ -155,13 +180,27 @@ __global__ void k_rowscan_part(PartArgs A) {
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < kThreads / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
-        if (MODE == 2) atomicAdd(A.outT + t, acc);
-        else atomicMax((unsigned long long*)(A.outT + t), as_bits(acc));  // non-negative doubles
+        A.part[c] = acc;
+    }
+}
+
+template <int MODE>
+__global__ void k_rowscan_part_fin(PartArgs A) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < A.nrows; t += (int64_t)gridDim.x * blockDim.x) {
+        double acc = 0.0;
+        for (int64_t c = A.row_chunk[t]; c < A.row_chunk[t + 1]; ++c) acc = MODE == 2 ? acc + A.part[c] : fmax(acc, A.part[c]);
+        A.outT[t] = acc;
     }
 }
 
 __global__ void k_scatter(const double* __restrict__ src, const int32_t* __restrict__ idx, double* __restrict__ dst,
                           int64_t k) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x)
+        dst[idx[t]] = src[t];
+}
+
+__global__ void k_scatter64(const double* __restrict__ src, const int64_t* __restrict__ idx, double* __restrict__ dst,
+                            int64_t k) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x)
         dst[idx[t]] = src[t];
 }
@@ -309,10 +348,6 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x)
 }
 // non-negative doubles compare like their bit patterns
 __device__ __forceinline__ double wave_max_abs(double v) { return as_double(wave_max_u64(as_bits(v))); }
-// argmax key: |v| with the 16 low mantissa bits replaced by (0xffff - i): ties -> smallest index
-__device__ __forceinline__ unsigned long long argmax_key(double av, int i) {
-    return (as_bits(av) & ~0xffffull) | (unsigned long long)(0xffff - i);
-}
 
 // Threshold pivot search (MUMPS/Duff-Reid rule, u then relaxed); run by one full wave, result
 // wave-uniform.  Mirrors test_pivot() of oracle/kkt_oracle.c; the relaxed ladder is only used at
@@ -336,15 +371,18 @@ __device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u
             minpiv = fmin(minpiv, fmax(acc, g));  // a larger null threshold would have stopped here
             if (acc != 0.0 && acc >= uu * g) { d.kind = PIV_1X1; d.c = c; d.relaxed = ul > 0; return d; }
             // 1x1 rejected: largest off-diagonal among the fully-summed rows is the 2x2 partner
-            unsigned long long key = 0;
+            // exact argmax, ties to the smallest row (oracle test_pivot: first strict maximum)
+            unsigned long long best = 0;
+            int bi = 0x7fffffff;
             for (int i = k + lane; i < p; i += 64) {
                 if (i == c) continue;
-                const double v = absA(st, i, c);
-                if (v > 0.0) key = umax64(key, argmax_key(v, i));
+                const unsigned long long b = as_bits(absA(st, i, c));
+                if (b > best) { best = b; bi = i; }  // rows ascending per lane: a tie keeps the smaller row
             }
-            key = wave_max_u64(key);
-            if (key != 0) {
-                const int r = 0xffff - (int)(key & 0xffffull);
+            const unsigned long long mx = wave_max_u64(best);
+            const unsigned long long ik = wave_max_u64(mx != 0 && best == mx ? 0xffffffffull - (unsigned)bi : 0ull);
+            if (mx != 0) {
+                const int r = (int)(0xffffffffull - ik);
                 double gc = 0.0, gr = 0.0;
                 for (int i = k + lane; i < m; i += 64) {
                     if (i == c || i == r) continue;
@@ -994,8 +1032,10 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 #pragma unroll
         for (int q = 0; q < EB; ++q) {
             const int64_t e = eb + (int64_t)q * NT;
-            const int lr = (int)(lp[q] >> 16), lc = (int)(lp[q] & 0xffffu);
-            const double v = sloc[lr] * uv[q] * sloc[lc];
+            const int lr = (int)(lp[q] >> 16), lc = (int)(lp[q] & 0x7fffu);
+            // the oracle's multiplication order (s of the larger original id first): bit-identical entries
+            const double sr = sloc[lr], sc = sloc[lc];
+            const double v = (lp[q] & 0x8000u) ? sc * uv[q] * sr : sr * uv[q] * sc;
             st.F[e < e1 ? st.idx(lr, lc) : -1] = v;
         }
         const int64_t nb = eb + (int64_t)EB * NT;
@@ -1934,7 +1974,8 @@ __global__ void k_xs_in(const double* __restrict__ b, const double* __restrict__
         xs[xpos[i]] = scale[i] * b[i];
 }
 __global__ void k_xs_out(const double* __restrict__ xs, const double* __restrict__ scale, const int32_t* __restrict__ xpos,
-                         double* __restrict__ x, int64_t n) {
+                         const uint32_t* __restrict__ abort_flag, double* __restrict__ x, int64_t n) {
+    if (*abort_flag) return;  // aborted dataflow solve: x (possibly aliasing the rhs) is left untouched
     for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
         x[i] = scale[i] * xs[xpos[i]];
 }
@@ -1981,20 +2022,35 @@ hipError_t launch_rowscan(const ScanArgs& A, int mode, hipStream_t s) {
         else hipLaunchKernelGGL(k_rowscan<2>, g, dim3(256), 0, s, A);
     }
     if (A.n_long > 0) {
-        const dim3 g((unsigned)((A.max_long + kLongChunk - 1) / kLongChunk), A.n_long);
-        if (mode == 0) hipLaunchKernelGGL(k_rowscan_long<0>, g, dim3(kThreads), 0, s, A);
-        else if (mode == 1) hipLaunchKernelGGL(k_rowscan_long<1>, g, dim3(kThreads), 0, s, A);
-        else hipLaunchKernelGGL(k_rowscan_long<2>, g, dim3(kThreads), 0, s, A);
+        const dim3 g((unsigned)A.long_chunks, A.n_long);
+        const dim3 gf((unsigned)((A.n_long + 63) / 64));
+        if (mode == 0) {
+            hipLaunchKernelGGL(k_rowscan_long<0>, g, dim3(kThreads), 0, s, A);
+            hipLaunchKernelGGL(k_rowscan_long_fin<0>, gf, dim3(64), 0, s, A);
+        } else if (mode == 1) {
+            hipLaunchKernelGGL(k_rowscan_long<1>, g, dim3(kThreads), 0, s, A);
+            hipLaunchKernelGGL(k_rowscan_long_fin<1>, gf, dim3(64), 0, s, A);
+        } else {
+            hipLaunchKernelGGL(k_rowscan_long<2>, g, dim3(kThreads), 0, s, A);
+            hipLaunchKernelGGL(k_rowscan_long_fin<2>, gf, dim3(64), 0, s, A);
+        }
     }
     return hipGetLastError();
 }
 
 hipError_t launch_rowscan_part(const PartArgs& A, int mode, hipStream_t s) {
-    if (A.nchunks <= 0) return hipSuccess;
-    const dim3 g((unsigned)A.nchunks);
-    if (mode == 0) hipLaunchKernelGGL(k_rowscan_part<0>, g, dim3(kThreads), 0, s, A);
-    else if (mode == 1) hipLaunchKernelGGL(k_rowscan_part<1>, g, dim3(kThreads), 0, s, A);
-    else hipLaunchKernelGGL(k_rowscan_part<2>, g, dim3(kThreads), 0, s, A);
+    if (A.nrows <= 0) return hipSuccess;
+    const dim3 g((unsigned)A.nchunks), gf((unsigned)grid_for(A.nrows, 256));
+    if (mode == 0) {
+        if (A.nchunks > 0) hipLaunchKernelGGL(k_rowscan_part<0>, g, dim3(kThreads), 0, s, A);
+        hipLaunchKernelGGL(k_rowscan_part_fin<0>, gf, dim3(256), 0, s, A);
+    } else if (mode == 1) {
+        if (A.nchunks > 0) hipLaunchKernelGGL(k_rowscan_part<1>, g, dim3(kThreads), 0, s, A);
+        hipLaunchKernelGGL(k_rowscan_part_fin<1>, gf, dim3(256), 0, s, A);
+    } else {
+        if (A.nchunks > 0) hipLaunchKernelGGL(k_rowscan_part<2>, g, dim3(kThreads), 0, s, A);
+        hipLaunchKernelGGL(k_rowscan_part_fin<2>, gf, dim3(256), 0, s, A);
+    }
     return hipGetLastError();
 }
 
@@ -2014,6 +2070,12 @@ hipError_t launch_normmax(const double* rowsum, const int32_t* list, int64_t n, 
 hipError_t launch_scatter(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_scatter, dim3(grid_for(k, 256)), dim3(256), 0, s, src, idx, dst, k);
+    return hipGetLastError();
+}
+
+hipError_t launch_scatter64(const double* src, const int64_t* idx, double* dst, int64_t k, hipStream_t s) {
+    if (k <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scatter64, dim3(grid_for(k, 256)), dim3(256), 0, s, src, idx, dst, k);
     return hipGetLastError();
 }
 
@@ -2191,9 +2253,10 @@ hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpo
     return hipGetLastError();
 }
 
-hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, double* x, int64_t n, hipStream_t s) {
+hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, const uint32_t* abort_flag, double* x,
+                         int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, x, n);
+    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, abort_flag, x, n);
     return hipGetLastError();
 }
 

@@ -14,7 +14,7 @@ struct FactorArgs {
     const int64_t* rows_off;    // nf+1
     const int32_t* rows;        // original ids, analysis order
     const int64_t* ent_off;     // nf+1 packed slot ranges
-    const uint32_t* ent_lpos;   // (lr << 16) | lc
+    const uint32_t* ent_lpos;   // (lr << 16) | flip << 15 | lc (flip: scale the column's side first)
     const double* uval;         // packed summed values
     const double* scale;        // equilibration, by original id
     const int32_t* child_off;   // nf+1
@@ -115,6 +115,8 @@ struct ScanArgs {
     const int32_t* long_rows;  // rows longer than kLongRow (new numbering)
     int32_t n_long;
     int64_t max_long;          // longest row length among long_rows
+    int64_t long_chunks;       // chunks of the longest long row (row stride of part)
+    double* part;              // n_long * long_chunks chunk results (combined in chunk order)
 };
 constexpr int kLongRow = 2048;
 
@@ -130,6 +132,9 @@ struct PartArgs {
     const double* uval;
     const double* scale;
     double* outT;                // per top row
+    int64_t nrows;               // top rows
+    const int64_t* row_chunk;    // nrows+1: chunks of top row t (consecutive in the chunk list)
+    double* part;                // nchunks chunk results (combined in chunk order, no atomics)
 };
 constexpr int kLongChunk = 4096;
 
@@ -148,6 +153,7 @@ hipError_t launch_scale_update(const double* rmax, double* scale, const int32_t*
 hipError_t launch_normmax(const double* rowsum, const int32_t* list, int64_t n, unsigned long long* anorm, hipStream_t s);
 hipError_t launch_scatter(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s);  // dst[idx[t]] = src[t]
 hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s);   // dst[t] = src[idx[t]]
+hipError_t launch_scatter64(const double* src, const int64_t* idx, double* dst, int64_t k, hipStream_t s);  // dst[idx[t]] = src[t]
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 // one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of
@@ -172,7 +178,8 @@ hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int ld
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, hipStream_t s);
 // xs[xpos[i]] = scale_i b_i  /  x_i = scale_i xs[xpos[i]]
 hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s);
-hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, double* x, int64_t n, hipStream_t s);
+hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, const uint32_t* abort_flag, double* x,
+                         int64_t n, hipStream_t s);
 
 constexpr int kMaxLdsFront = 128;
 constexpr int kMaxWaveFront = 72;     // one-wave register-resident factorization (8 x 8 lane grid, 9 row blocks)     // fronts up to this order factor entirely in LDS
