@@ -10,7 +10,10 @@ from kkt_cases import null_threshold_case
 from oracle_ffi import OracleKKT
 
 N_HUB = 800_000          # ||A_pre||_inf = 1 + N/2 -> k* = 4.00001 (3 sweeps), 0.50001 (1 sweep)
-KS = [2, 8, 3, 5, 1, 16]  # 0.5x, 2x, 0.75x, 1.25x, 0.25x, 4x the threshold
+# 0.5x, 2x, 1.5x, 4x and 0.99999x the threshold.  Even k only: the second pivot is then exactly -k eps in
+# either elimination order (1 / (1 - k eps) rounds to 1 + k eps), so the decision cannot depend on the
+# ordering (the product's nested dissection and the oracle's RCM differ)
+KS = [2, 8, 6, 16, 4]
 
 
 @pytest.mark.parametrize("block_scale", [1.0, 2.0 ** 30, 2.0 ** -30])
@@ -43,6 +46,14 @@ def test_gpu_threshold_matches_oracle(block_scale, overlap_norm):
     o.analyze(n, r, c)
     o.factorize(v)
     assert g.inertia() == o.inertia() == inertia
-    # the solve: null pivots contribute 0 (MUMPS ICNTL(24) semantics) in both
+    # the solve: null pivots contribute 0 (MUMPS ICNTL(24) semantics).  Which row of a singular block is
+    # the null pivot depends on the elimination order (product: nested dissection, oracle: RCM), so the
+    # two "solutions" of a singular block may differ; every other row must agree
     b = np.cos(np.arange(n, dtype=np.float64))
-    np.testing.assert_allclose(g.solve(b), o.solve(b), rtol=1e-10, atol=1e-12)
+    xg, xo = g.solve(b), o.solve(b)
+    keep = np.ones(n, bool)
+    for t, k in enumerate(KS):
+        if k <= 4:  # null blocks (k* = 4.00001)
+            keep[1 + N_HUB + 2 * t: 3 + N_HUB + 2 * t] = False
+    np.testing.assert_allclose(xg[keep], xo[keep], rtol=1e-10, atol=1e-12)
+    assert np.isfinite(xg).all()

@@ -123,6 +123,7 @@ struct uno_kkt {
     int delay_relaxed = 1;      // also amalgamate fronts whose pivots needed a relaxed threshold (MUMPS: delay)
     int max_merge_rounds = 64;
     int verbose = 0;
+    std::chrono::steady_clock::time_point t_factor;  // verbose >= 2: per-factorization wall time
     int64_t merges_total = 0;
     bool analyzed = false, factor_enqueued = false, factored = false;
     const double* values_ptr = nullptr;  // device values used by the last factorization
@@ -133,6 +134,9 @@ struct uno_kkt {
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
     DBuf<int32_t> ch_cm;
     DBuf<int8_t> piv;
+    DBuf<BigFrontState> big;              // large-front factorization state (fronts with m > kMaxLdsFront)
+    DBuf<int32_t> big_pending;
+    int32_t* h_big = nullptr;             // pinned: fronts still factoring (run_big_fronts)
     DBuf<unsigned long long> anorm, counters, stamps, fcnt, minbits;
     DBuf<double> fmin;
     int want_stamps = 0;
@@ -255,6 +259,33 @@ void flush_timing(uno_kkt_t h) {
 
 int upload_structure(uno_kkt_t h);
 int enqueue_factorization(uno_kkt_t h);
+
+// Fronts beyond LDS (m > kMaxLdsFront): blocked factorization in HBM scratch (kkt_kernels.hip k_big_*).
+// Every panel + update step advances each unfinished front by at least one pivot; the host queues
+// batches of steps and checks (one small copy + stream sync per batch) until no front is left.
+int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
+
+int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
+    if (count <= 0) return UNO_KKT_OK;
+    HIPCHK(h, launch_big_assemble(A, fronts, count, mmax, s));
+    const int nb = big_panel_width();
+    int batch = (mmax + nb - 1) / nb + 2;
+    int64_t steps = 0;
+    for (;;) {
+        for (int r = 0; r < batch; ++r) HIPCHK(h, launch_big_step(A, fronts, count, mmax, s));
+        steps += batch;
+        HIPCHK(h, launch_big_pending(A, fronts, count, h->big_pending.p, s));
+        HIPCHK(h, hipMemcpyAsync(h->h_big, h->big_pending.p, sizeof(int32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        if (*h->h_big == 0) break;
+        if (steps > 2 * (int64_t)mmax + 64)
+            return set_err(h, UNO_KKT_ERR_HIP, "internal: large-front factorization made no progress");
+        batch = 8;  // early panel stops (interchanges, 2x2 / null pivots): a few more steps
+    }
+    HIPCHK(h, launch_big_finish(A, fronts, count, mmax, s));
+    if (h->verbose >= 2) fprintf(stderr, "[uno_kkt] large fronts: %d of order <= %d, %lld panel steps\n", count, mmax, (long long)steps);
+    return UNO_KKT_OK;
+}
 
 DfArgs dataflow_args(uno_kkt_t h) {
     DfArgs D;
@@ -657,12 +688,18 @@ int finish_factorization(uno_kkt_t h) {
         h->factor_enqueued = false;
         if (h->verbose)
             fprintf(stderr, "[uno_kkt] merge round %d: %lld delayed columns listed, %lld moved, stuck %llu; "
-                            "rebuild %.3f s, upload %.3f s, refactor %.3f s, fronts %lld\n", round, (long long)dv.size(),
+                            "rebuild %.3f s, upload %.3f s, refactor %.3f s, fronts %lld, max front %lld\n", round, (long long)dv.size(),
                     (long long)moved, (unsigned long long)c[5],
                     std::chrono::duration<double>(tu - tb).count() - 0.0,
-                    0.0, std::chrono::duration<double>(std::chrono::steady_clock::now() - tu).count(), (long long)h->S.nf);
+                    0.0, std::chrono::duration<double>(std::chrono::steady_clock::now() - tu).count(), (long long)h->S.nf,
+                    (long long)h->S.max_m);
     }
     const unsigned long long* c = h->h_counters;
+    if (h->verbose >= 2)
+        fprintf(stderr, "[uno_kkt] factorization %lld: %.3f ms (enqueue to checked), inertia (%llu, %llu, %llu), merges %lld\n",
+                (long long)h->st.factorizations,
+                std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - h->t_factor).count(), c[0], c[1],
+                c[2], (long long)h->merges_total);
     h->st.pivots_2x2 = (int64_t)c[3];
     h->st.pivots_null = (int64_t)c[2];
     h->st.pivots_relaxed = (int64_t)c[4];
@@ -907,6 +944,8 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->cb.alloc(S.cb_size));
     HIPCHK(h, h->cvec.alloc(S.f_relmap_off.empty() ? 0 : S.f_relmap_off.back()));
     HIPCHK(h, h->gscratch.alloc(gtot));
+    HIPCHK(h, h->big.alloc(S.max_m > kMaxLdsFront ? S.nf : 0));
+    if (!h->big_pending.p) HIPCHK(h, h->big_pending.alloc(1));
     HIPCHK(h, h->frow.alloc(S.rows.size()));
     HIPCHK(h, h->fpos.alloc(S.rows.size()));
     HIPCHK(h, h->piv.alloc(S.rows.size()));
@@ -1001,6 +1040,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
+    A.big = h->big.p;
     if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     A.stamps = nullptr;
@@ -1025,7 +1065,12 @@ int enqueue_factorization(uno_kkt_t h) {
         for (size_t u = q; u < r; ++u) {
             const Launch& L = lp.fac[u];
             hipStream_t ls = (u > q && h->concurrent_classes) ? h->stream3 : s;
-            HIPCHK(h, launch_factor(A, lp.fac_fronts.p + L.begin, L.count, L.mmax, L.global, ls));
+            if (L.global) {
+                const int rc = run_big_fronts(h, A, lp.fac_fronts.p + L.begin, L.count, L.mmax, ls);
+                if (rc != UNO_KKT_OK) return rc;
+            } else {
+                HIPCHK(h, launch_factor(A, lp.fac_fronts.p + L.begin, L.count, L.mmax, false, ls));
+            }
         }
         if (r - q > 1 && h->concurrent_classes) {
             HIPCHK(h, hipEventRecord(h->ev_join, h->stream3));
@@ -1052,7 +1097,12 @@ int enqueue_factorization(uno_kkt_t h) {
         if (rc != UNO_KKT_OK) return rc;
         for (const Launch& L : h->plan[1].fac) {
             TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
-            HIPCHK(h, launch_factor(A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, L.global, s));
+            if (L.global) {
+                rc = run_big_fronts(h, A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, s);
+                if (rc != UNO_KKT_OK) return rc;
+            } else {
+                HIPCHK(h, launch_factor(A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, false, s));
+            }
         }
     }
     HIPCHK(h, hipMemsetAsync(h->minbits.p, 0xff, 8, s));
@@ -1091,12 +1141,27 @@ int uno_kkt_create(uno_kkt_t* handle, int device_id) {
         hipEventCreateWithFlags(&h->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_scale, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_norm, hipEventDisableTiming) != hipSuccess ||
-        hipHostMalloc((void**)&h->h_counters, 12 * sizeof(unsigned long long)) != hipSuccess) {
+        hipHostMalloc((void**)&h->h_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
+        hipHostMalloc((void**)&h->h_big, sizeof(int32_t)) != hipSuccess) {
         delete h;
         return UNO_KKT_ERR_HIP;
     }
     memset(h->h_counters, 0, 12 * sizeof(unsigned long long));
+    if (const char* v = getenv("UNO_KKT_VERBOSE")) h->verbose = atoi(v);  // diagnostics of embedded uses
     *handle = h;
+    // UNO_KKT_OPTIONS="name=value,name=value": options for embedded uses (the Uno plugin has no option path)
+    if (const char* o = getenv("UNO_KKT_OPTIONS")) {
+        std::string all(o);
+        size_t b = 0;
+        while (b < all.size()) {
+            size_t e = all.find(',', b);
+            if (e == std::string::npos) e = all.size();
+            const std::string kv = all.substr(b, e - b);
+            const size_t eq = kv.find('=');
+            if (eq != std::string::npos) uno_kkt_set_option(h, kv.substr(0, eq).c_str(), atof(kv.c_str() + eq + 1));
+            b = e + 1;
+        }
+    }
     return UNO_KKT_OK;
 }
 
@@ -1107,6 +1172,7 @@ void uno_kkt_destroy(uno_kkt_t h) {
     for (auto& t : h->pending) { hipEventDestroy(t.a); hipEventDestroy(t.b); }
     for (auto e : h->ev_pool) hipEventDestroy(e);
     if (h->h_counters) hipHostFree(h->h_counters);
+    if (h->h_big) hipHostFree(h->h_big);
     if (h->stream2) hipStreamSynchronize(h->stream2);
     if (h->ev_scale) hipEventDestroy(h->ev_scale);
     if (h->ev_norm) hipEventDestroy(h->ev_norm);
@@ -1256,6 +1322,7 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
             HIPCHK(h, hipMemcpyAsync(h->values.p, values, S.nnz * sizeof(double), hipMemcpyHostToDevice, h->stream));
         h->values_ptr = h->values.p;
     }
+    h->t_factor = std::chrono::steady_clock::now();
     int rc = enqueue_factorization(h);
     if (rc != UNO_KKT_OK) return rc;
     h->packed_valid = h->world == 1;  // one GPU packs every slot

@@ -5,7 +5,7 @@
 //   k_pack          COO values -> packed per-front slots (duplicates summed, MUMPS sym=2), row maxima
 //   k_scale*        symmetric infinity-norm equilibration (ICNTL(8)=8 restated), ||A_pre||_inf
 //   k_factor_lds<MR> one workgroup per front: assemble + extend-add + threshold 1x1/2x2 LDL^T in LDS
-//   k_factor_global  same algorithm for fronts too large for LDS (front lives in HBM scratch)
+//   k_big_*          blocked LDL^T of fronts too large for LDS (HBM scratch, MFMA f64 trailing updates)
 //   k_solve_fwd / k_solve_bwd  level-scheduled multifrontal triangular solves (nrhs = 1)
 // Every front is processed by one 256-thread workgroup (4 waves of 64); pivot search runs in wave 0
 // with butterfly shuffles, the rank-1/rank-2 Schur updates are spread over a 16x16 thread grid.
@@ -1180,21 +1180,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     if (par >= 0 && threadIdx.x == 0) __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-__global__ __launch_bounds__(kThreads) void k_factor_global(FactorArgs A, const int32_t* __restrict__ fronts) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
-    const int f = fronts[blockIdx.x];
-    const int m = A.fm[f], p = A.fp[f];
-    const FullStore st{A.gscratch + A.gscratch_off[f], m};
-    double* sloc = smem + 4;
-    double* coefB = sloc + m;
-    int32_t* lrow = (int32_t*)(coefB + m);
-    int32_t* rstage = lrow + m;
-    int8_t* pk = (int8_t*)(rstage + m);
-    assemble_front<kThreads, false>(st, (int64_t)m * m, m, p, lrow, sloc, rstage, A, f);
-    factor_front<kThreads, 0, false>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
-}
-
 // ------------------------------------------------------------------------------------------------
 // triangular solves (multifrontal, level by level)
 // ------------------------------------------------------------------------------------------------
@@ -1996,6 +1981,327 @@ __global__ __launch_bounds__(64) void k_xpos(SolveArgs A, DfArgs D, int32_t* __r
 }
 
 // ------------------------------------------------------------------------------------------------
+// large fronts (m > kMaxLdsFront): blocked LDL^T in HBM scratch, trailing updates on MFMA f64
+// ------------------------------------------------------------------------------------------------
+// The front lives in its FullStore (row-major, lower triangle used) and is factored in panels of at most
+// kBigNB pivots by a sequence of batched launches over the large fronts of one level:
+//   k_big_assemble  original entries + children's contribution blocks (assemble_front), row ids
+//   k_big_panel     one block per front: pivots of the next panel.  Column k is brought up to date
+//                   left-looking (minus the panel's earlier pivots, L(i,q) W(k,q)), then tested with the
+//                   threshold rule; a pass is a 1x1 pivot.  On a failure with pivots pending the panel
+//                   ends (the trailing update must land first); on a failure at the panel's start every
+//                   column is current and the exact full search of the small-front kernels runs
+//                   (search_pivot: interchanges, 2x2, null pivots, relaxed ladder) -- so the pivot
+//                   sequence follows the same rule as factor_front / the oracle.
+//   k_big_update    C -= L21 W21^T over the trailing lower triangle, W = the unnormalised pivot columns
+//                   (= L D), on v_mfma_f64_16x16x4f64: 64 x 64 macro tiles, one 16-row strip per wave.
+//   k_big_finish    L (packed trapezoid), pivoted row maps, contribution block, pivot counters.
+// The host repeats panel + update until every front of the launch is done (one check per batch).
+constexpr int kBigNB = 32;
+
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// L(i, q) = ca * W(i, base) + cb * W(i, base + 1): the write-out coefficients of factor_front
+template <class S>
+__device__ __forceinline__ void piv_coefs(const S& st, const int8_t* piv, int q, double& ca, double& cb, int& base) {
+    const int8_t kind = piv[q];
+    ca = 0.0; cb = 0.0; base = q;
+    if (kind == PIV_1X1) {
+        ca = 1.0 / st.at(q, q);
+    } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+        const int k0 = kind == PIV_2X2_A ? q : q - 1;
+        const double a = st.at(k0, k0), b = st.at(k0 + 1, k0), e = st.at(k0 + 1, k0 + 1);
+        const double idet = 1.0 / (a * e - b * b);
+        if (kind == PIV_2X2_A) { ca = e * idet; cb = -b * idet; }
+        else { ca = -b * idet; cb = a * idet; }
+        base = k0;
+    }
+}
+
+__device__ __forceinline__ double block_max256(double v, double* red) {
+    v = wave_max_abs(v);  // non-negative values
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+    __syncthreads();
+    const double r = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+    __syncthreads();
+    return r;
+}
+
+__global__ __launch_bounds__(kThreads) void k_big_assemble(FactorArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    double* sloc = smem;
+    int32_t* lrow = (int32_t*)(sloc + m);
+    assemble_front<kThreads, false>(st, (int64_t)m * m, m, p, lrow, sloc, lrow, A, f);
+    const int64_t ro = A.rows_off[f];
+    for (int i = threadIdx.x; i < m; i += kThreads) {
+        A.frow[ro + i] = lrow[i];  // row ids, permuted in place by the interchanges
+        A.fpos[ro + i] = i;        // analysis-order local row of position i (inverted by k_big_finish)
+    }
+    if (threadIdx.x == 0) {
+        BigFrontState z{};
+        z.done = p == 0;
+        z.minpiv = INFINITY;
+        A.big[f] = z;
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_big_panel(FactorArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double colbuf[];  // column k brought up to date (m doubles)
+    __shared__ double wk[kBigNB + 2], cA[kBigNB + 2], cB[kBigNB + 2], red[4];
+    __shared__ int bq[kBigNB + 2];
+    __shared__ BigFrontState S;
+    __shared__ FrontShared sh;
+    const int tid = threadIdx.x;
+    const int f = fronts[blockIdx.x];
+    if (tid == 0) S = A.big[f];
+    __syncthreads();
+    if (S.done) {  // the last panel's update has been applied: nothing pending for k_big_update
+        if (tid == 0 && S.k1 != S.k0) { A.big[f].k0 = S.k1; }
+        return;
+    }
+    const int m = A.fm[f], p = A.fp[f];
+    const int64_t ro = A.rows_off[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    int32_t* lrow = A.frow + ro;
+    int32_t* lorig = A.fpos + ro;
+    int8_t* piv = A.piv + ro;
+    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+    double minpiv = S.minpiv;  // wave 0 keeps it (uniform)
+    const int k0 = S.k;
+    int k = k0;
+    while (k < p && k - k0 < kBigNB) {
+        const int np = k - k0;
+        // left-looking: column k minus the panel's pivots, into colbuf (the store keeps the stale column
+        // until the pivot is accepted: a panel that stops here leaves it to k_big_update)
+        for (int q = tid; q < np; q += kThreads) wk[q] = st.at(k, k0 + q);
+        __syncthreads();
+        for (int i = k + tid; i < m; i += kThreads) {
+            double acc = st.at(i, k);
+            for (int q = 0; q < np; ++q) {
+                double l = cA[q] * st.at(i, bq[q]);
+                if (cB[q] != 0.0) l += cB[q] * st.at(i, bq[q] + 1);
+                acc -= l * wk[q];
+            }
+            colbuf[i] = acc;
+        }
+        __syncthreads();
+        const double akk = colbuf[k];
+        double g = 0.0;
+        for (int i = k + 1 + tid; i < m; i += kThreads) g = fmax(g, fabs(colbuf[i]));
+        g = block_max256(g, red);
+        const double aak = fabs(akk);
+        if (aak > thres && !(A.u * g > aak)) {  // 1x1 pivot at k without interchange (quick test)
+            for (int i = k + tid; i < m; i += kThreads) st.at(i, k) = colbuf[i];
+            if (tid == 0) {
+                piv[k] = PIV_1X1;
+                if (akk > 0.0) S.npos++; else S.nneg++;
+                cA[np] = 1.0 / akk; cB[np] = 0.0; bq[np] = k;
+            }
+            minpiv = fmin(minpiv, aak);
+            __syncthreads();
+            k += 1;
+            continue;
+        }
+        if (np > 0) break;  // the trailing update must land before a full search
+        // panel start: every column is current -> the exact search of the small-front kernels
+        if (tid < 64) {
+            const PivotDecision d = search_pivot(st, m, k, p, A.u, thres, minpiv);
+            if (tid == 0) sh.dec = d;
+        }
+        __syncthreads();
+        PivotDecision d = sh.dec;
+        if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
+        if (d.c != k) {
+            sym_swap<kThreads>(st, m, k, d.c, lrow, lorig);
+            __syncthreads();
+        }
+        if (d.kind == PIV_2X2_A) {
+            const int r = d.r == k ? d.c : d.r;
+            if (r != k + 1) {
+                sym_swap<kThreads>(st, m, k + 1, r, lrow, lorig);
+                __syncthreads();
+            }
+        }
+        if (tid == 0) {
+            if (sh.dec.kind == PIV_STUCK) S.nstuck++;
+            S.nrel += d.relaxed;
+            if (d.relaxed && !S.delays && A.record_delays && A.fparent[f] >= 0) {  // see factor_front
+                S.delays = 1;
+                const unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
+                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
+            }
+        }
+        if (d.kind == PIV_NULL) {
+            for (int i = k + 1 + tid; i < m; i += kThreads) st.at(i, k) = 0.0;
+            if (tid == 0) { piv[k] = PIV_NULL; S.nzero++; cA[0] = 0.0; cB[0] = 0.0; bq[0] = k; }
+            __syncthreads();
+            k += 1;
+        } else if (d.kind == PIV_1X1) {
+            if (tid == 0) {
+                const double dk = st.at(k, k);
+                piv[k] = PIV_1X1;
+                if (dk > 0.0) S.npos++; else S.nneg++;
+                cA[0] = 1.0 / dk; cB[0] = 0.0; bq[0] = k;
+            }
+            __syncthreads();
+            k += 1;
+        } else {  // 2x2 on (k, k+1)
+            if (tid == 0) {
+                const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
+                const double det = a * e - b * b, idet = 1.0 / det;
+                piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; S.n2++;
+                if (det < 0.0) { S.npos++; S.nneg++; }
+                else if (a + e > 0.0) S.npos += 2;
+                else S.nneg += 2;
+                cA[0] = e * idet; cB[0] = -b * idet; bq[0] = k;
+                cA[1] = -b * idet; cB[1] = a * idet; bq[1] = k;
+            }
+            __syncthreads();
+            k += 2;
+        }
+    }
+    if (tid == 0) {
+        S.minpiv = minpiv;
+        S.k0 = k0;
+        S.k1 = k;
+        S.k = k;
+        S.done = k >= p;
+        A.big[f] = S;
+    }
+}
+
+// Trailing update of the pending panel [k0, k1): rows / columns [k1, m), lower triangle.  Block = one
+// 64 x 64 macro tile (blockIdx.x, lower-triangular order) of front fronts[blockIdx.y]; wave w owns rows
+// 16w .. 16w+15 of it and four 16 x 16 MFMA accumulators along the columns.
+__global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int32_t* __restrict__ fronts) {
+    __shared__ double cA[kBigNB + 2], cB[kBigNB + 2];
+    __shared__ int bq[kBigNB + 2];
+    const int f = fronts[blockIdx.y];
+    const BigFrontState S = A.big[f];
+    const int k0 = S.k0, k1 = S.k1;
+    if (k1 <= k0) return;
+    const int m = A.fm[f];
+    const int nt = (m - k1 + 63) / 64;
+    if ((int)blockIdx.x >= nt * (nt + 1) / 2) return;
+    int ti, tj;
+    tri_rc((int)blockIdx.x, ti, tj);
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const int8_t* piv = A.piv + A.rows_off[f];
+    const int np = k1 - k0;
+    for (int q = threadIdx.x; q < np; q += kThreads) {
+        double ca, cb;
+        int b;
+        piv_coefs(st, piv, k0 + q, ca, cb, b);
+        cA[q] = ca; cB[q] = cb; bq[q] = b;
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int i0 = k1 + 64 * ti + 16 * w;
+    const int lr = lane & 15, lk = lane >> 4;
+    dbl4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int j0 = k1 + 64 * tj + 16 * c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + lk + 4 * r, j = j0 + lr;
+            acc[c][r] = (i < m && j < m && j <= i) ? st.at(i, j) : 0.0;
+        }
+    }
+    const bool diag = ti == tj;
+    const int ia = i0 + lr;  // A-operand row of this lane
+    for (int q = 0; q < np; q += 4) {
+        const int qq = q + lk;
+        double a = 0.0;
+        if (qq < np && ia < m) {
+            a = cA[qq] * st.at(ia, bq[qq]);
+            if (cB[qq] != 0.0) a += cB[qq] * st.at(ia, bq[qq] + 1);
+            a = -a;
+        }
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (diag && c > w) continue;  // wave-uniform: strip entirely above the diagonal
+            const int jb = k1 + 64 * tj + 16 * c + lr;  // B-operand column of this lane
+            const double b = (qq < np && jb < m) ? st.at(jb, k0 + qq) : 0.0;
+            acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (diag && c > w) continue;
+        const int j0 = k1 + 64 * tj + 16 * c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + lk + 4 * r, j = j0 + lr;
+            if (i < m && j < m && j <= i) st.at(i, j) = acc[c][r];
+        }
+    }
+}
+
+// fronts of a launch still factoring (host loop condition)
+__global__ void k_big_pending(const FactorArgs A, const int32_t* __restrict__ fronts, int count, int32_t* __restrict__ out) {
+    int n = 0;
+    for (int t = threadIdx.x; t < count; t += blockDim.x) n += A.big[fronts[t]].done ? 0 : 1;
+    for (int off = 32; off > 0; off >>= 1) n += __shfl_xor(n, off);
+    __shared__ int red[4];
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = n;
+    __syncthreads();
+    if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
+}
+
+__global__ __launch_bounds__(kThreads) void k_big_finish(FactorArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    int32_t* lorig = (int32_t*)smem;
+    const int tid = threadIdx.x;
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int64_t ro = A.rows_off[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const int8_t* piv = A.piv + ro;
+    // L: packed lower trapezoid, column j rows j..m-1; one wave per column (coalesced stores)
+    double* L = A.L + A.L_off[f];
+    const int lane = tid & 63;
+    for (int j = tid >> 6; j < p; j += kThreads / 64) {
+        double ca, cb;
+        int base;
+        piv_coefs(st, piv, j, ca, cb, base);
+        const int8_t kind = piv[j];
+        double* Lj = L + (int64_t)j * m - (int64_t)j * (j - 1) / 2 - j;  // L(i, j) = Lj[i]
+        for (int i = j + lane; i < m; i += 64) {
+            double v;
+            if (i == j) v = kind == PIV_NULL ? 0.0 : st.at(j, j);
+            else if (kind == PIV_2X2_A && i == j + 1) v = st.at(j + 1, j);  // D off-diagonal
+            else {
+                v = ca * st.at(i, base);
+                if (kind >= PIV_2X2_A) v += cb * st.at(i, base + 1);
+            }
+            Lj[i] = v;
+        }
+    }
+    // analysis-order local row -> pivoted position
+    for (int i = tid; i < m; i += kThreads) lorig[i] = A.fpos[ro + i];
+    __syncthreads();
+    for (int i = tid; i < m; i += kThreads) A.fpos[ro + lorig[i]] = i;
+    // contribution block: row-major packed lower triangle of order m - p
+    const int cm = m - p;
+    if (cm > 0) {
+        double* cb = A.cb + A.cb_off[f];
+        for (int r = tid >> 6; r < cm; r += kThreads / 64)
+            for (int c = lane; c <= r; c += 64) cb[(int64_t)r * (r + 1) / 2 + c] = st.at(p + r, p + c);
+    }
+    if (tid == 0) {
+        const BigFrontState S = A.big[f];
+        A.fstat[f] = (int32_t)((S.nstuck > 0xffff ? 0xffff : S.nstuck) | ((S.nrel > 0x7fff ? 0x7fff : S.nrel) << 16));
+        A.fcnt[f] = (unsigned long long)S.npos | (unsigned long long)S.nneg << 16 | (unsigned long long)S.nzero << 32 |
+                    (unsigned long long)S.n2 << 48;
+        A.fmin[f] = S.minpiv;
+    }
+}
+
+// ------------------------------------------------------------------------------------------------
 // host-side launch helpers
 // ------------------------------------------------------------------------------------------------
 
@@ -2124,8 +2430,7 @@ size_t factor_lds_bytes(int mmax) {
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (global) {
-        size_t sh = 32 + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) + (size_t)((mmax + 15) & ~15);
-        hipLaunchKernelGGL(k_factor_global, dim3(count), dim3(kThreads), sh, s, A, fronts);
+        return hipErrorInvalidValue;  // fronts beyond LDS: launch_big_* (host loop in kkt_api.cpp)
     } else {
         size_t sh = factor_lds_bytes(mmax);
         // small fronts: one wave per front (no cross-wave barriers, more fronts per CU);
@@ -2215,6 +2520,34 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
     else hipLaunchKernelGGL(k_solve_bwd_w, dim3(count), dim3(64), sh, s, A, fronts);
     return hipGetLastError();
 }
+
+hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    const size_t sh = (size_t)mmax * (sizeof(double) + sizeof(int32_t)) + 16;
+    hipLaunchKernelGGL(k_big_assemble, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    return hipGetLastError();
+}
+
+hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_big_panel, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(double) + 16, s, A, fronts);
+    const int nt = (mmax + 63) / 64;
+    hipLaunchKernelGGL(k_big_update, dim3(nt * (nt + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
+    return hipGetLastError();
+}
+
+hipError_t launch_big_pending(const FactorArgs& A, const int32_t* fronts, int count, int32_t* out, hipStream_t s) {
+    hipLaunchKernelGGL(k_big_pending, dim3(1), dim3(256), 0, s, A, fronts, count, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_big_finish, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(int32_t) + 16, s, A, fronts);
+    return hipGetLastError();
+}
+
+int big_panel_width() { return kBigNB; }
 
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     if (A.df_nf <= 0) return hipSuccess;

@@ -7,6 +7,15 @@
 
 namespace ukkt {
 
+// Per-front state of the blocked large-front factorization (kkt_kernels.hip k_big_*), by front id.
+struct BigFrontState {
+    int32_t k;          // next pivot position
+    int32_t k0, k1;     // pivots of the last panel: [k0, k1) (its trailing update is applied by k_big_update)
+    int32_t done;
+    int32_t npos, nneg, nzero, n2, nrel, nstuck, delays, pad;
+    double minpiv;      // smallest pivot magnitude accepted as non-null
+};
+
 // Arguments of the front factorization kernels (device pointers, SoA per front).
 struct FactorArgs {
     const int32_t* fm;          // front order
@@ -53,6 +62,7 @@ struct FactorArgs {
     uint32_t df_epoch;          // 1, 2, ... per factorization since the counters were cleared
     uint32_t* df_ticket;        // block start order (cumulative: (epoch - 1) * df_nf at launch)
     uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
+    BigFrontState* big;         // per front: state of the blocked large-front factorization (m > kMaxLdsFront)
 };
 
 struct SolveArgs {
@@ -167,6 +177,14 @@ hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
                         hipStream_t s);
+
+// blocked large fronts (m > kMaxLdsFront): assemble, then (panel + MFMA trailing update) steps until
+// launch_big_pending reports no front still factoring, then finish (L, CB, row maps, counters)
+hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
+hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
+hipError_t launch_big_pending(const FactorArgs& A, const int32_t* fronts, int count, int32_t* out, hipStream_t s);
+hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
+int big_panel_width();
 
 // dataflow factorization of the upper tree (one-wave fronts, m <= 64)
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
