@@ -1,6 +1,8 @@
 // HIPLDLSolver.cpp -- see HIPLDLSolver.hpp.  Each method names the MUMPS call it replaces.
 #include "HIPLDLSolver.hpp"
 
+#include <cstdlib>
+#include <cstring>
 #include <stdexcept>
 #include <string>
 
@@ -13,7 +15,15 @@ namespace uno {
    namespace {
       void* hip_create() {
          uno_kkt_t h = nullptr;
-         return uno_kkt_create(&h, 0) == UNO_KKT_OK ? h : nullptr;
+         if (uno_kkt_create(&h, 0) != UNO_KKT_OK) return nullptr;
+         // Inside an interior-point solve the values change at every factorization, so delayed pivots
+         // (MUMPS passes them to the parent front within JOB=2) would cost the library a re-analysis per
+         // new delay.  The plugin therefore relaxes the pivot threshold inside the front instead (ladder
+         // u, u/10, u/100, 1e-6, 1e-10) and the library follows such a factorization with one step of
+         // iterative refinement (option "refine").  UNO_KKT_OPTIONS=delay_relaxed=1 restores the delays.
+         const char* env = std::getenv("UNO_KKT_OPTIONS");
+         if (env == nullptr || std::strstr(env, "delay_relaxed") == nullptr) uno_kkt_set_option(h, "delay_relaxed", 0.0);
+         return h;
       }
       void hip_destroy(void* h) { uno_kkt_destroy(static_cast<uno_kkt_t>(h)); }
       int hip_analyze(void* h, int64_t n, int64_t nnz, const int64_t* r, const int64_t* c) {

@@ -260,3 +260,25 @@ def test_c3_full_size(uno_amd):
     np.testing.assert_allclose(xg, o.solve(b), rtol=1e-6, atol=1e-9 * np.abs(xg).max())
     st = g.stats()
     assert st["solve_aborts"] == 0 and st["factor_df_aborts"] == 0
+
+
+def test_threshold_relaxation_with_refinement(uno_amd):
+    """delay_relaxed = 0 (the Uno plugin's setting, integration/HIPLDLSolver.cpp): a front whose fully-summed
+    block has no pivot passing u relaxes the threshold instead of delaying the columns to its parent (no
+    re-analysis); the factorization is then followed by one step of iterative refinement.  Inertia equal
+    to the oracle's (which delays, as MUMPS); residual within the 1e-10 bar after refinement."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(10000, SEEDS["C2"])
+    g, o = both(n, r, c, v, delay_relaxed=0)
+    assert g.inertia() == o.inertia()
+    st = g.stats()
+    assert st["pivots_relaxed"] > 0 and st["fronts_merged"] == 0
+    xg = g.solve(b)
+    assert rel_residual(n, r, c, v, xg, b) < RES_TOL
+    np.testing.assert_allclose(xg, o.solve(b), rtol=1e-6, atol=1e-9 * np.abs(xg).max())
+    # aliasing device solve with refinement keeps the right-hand side for the residual
+    import torch
+    bd = torch.from_numpy(b.copy()).to("cuda")
+    g.solve_device(bd.data_ptr(), bd.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_allclose(bd.cpu().numpy(), xg, rtol=1e-12, atol=1e-14 * np.abs(xg).max())

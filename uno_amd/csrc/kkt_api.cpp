@@ -179,6 +179,8 @@ struct uno_kkt {
     DBuf<int32_t> jv_ent, j_con;
     DBuf<unsigned long long> alpha;
     DBuf<double> symv_tmp, symv_part, dot_d;
+    DBuf<double> xtmp, rtmp;              // host-pointer solves / refinement residuals
+    int refine = 1;                       // refinement steps after a factorization with relaxed pivots
     DBuf<int64_t> edit_pos;               // uno_kkt_set_values staging
     DBuf<double> edit_val;
     bool packed_valid = false;            // uval holds the current values (symv reuses the factor's pack)
@@ -259,6 +261,7 @@ void flush_timing(uno_kkt_t h) {
 
 int upload_structure(uno_kkt_t h);
 int enqueue_factorization(uno_kkt_t h);
+int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* dot);
 
 // Fronts beyond LDS (m > kMaxLdsFront): blocked factorization in HBM scratch (kkt_kernels.hip k_big_*).
 // Every panel + update step advances each unfinished front by at least one pivot; the host queues
@@ -939,6 +942,8 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, h->rmax.alloc(n));
         HIPCHK(h, h->w.alloc(n));
         HIPCHK(h, h->bvec.alloc(n));
+        HIPCHK(h, h->xtmp.alloc(n));
+        HIPCHK(h, h->rtmp.alloc(n));
     }
     HIPCHK(h, h->L.alloc(S.L_size));
     HIPCHK(h, h->cb.alloc(S.cb_size));
@@ -1196,6 +1201,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "dense_factor") h->aopt.dense_factor = value;
     else if (n == "timing") h->timing = value != 0.0;
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
+    else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else if (n == "gather_solution") h->gather_solution = value != 0.0;
@@ -1341,22 +1347,15 @@ int uno_kkt_inertia(uno_kkt_t h, int64_t* positive, int64_t* negative, int64_t* 
     return UNO_KKT_OK;
 }
 
-int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
-    if (!h || !rhs || !x) return UNO_KKT_ERR_ARG;
-    if (!h->analyzed || (!h->factored && !h->factor_enqueued))
-        return set_err(h, UNO_KKT_ERR_STATE, "solve before factorize");
-    HIPCHK(h, hipSetDevice(h->device));
+}  // extern "C"
+
+namespace {
+// One solve with the last factorization, device pointers (b may alias xd: b is read by the first kernel,
+// xd written by the last).  Returns after the stream has drained when the dataflow solve ran (its abort
+// flag is checked in the same call).
+int solve_core(uno_kkt_t h, const double* b, double* xd) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
-    if (h->factor_enqueued) {  // the factorization is final only once checked (delays, null threshold)
-        int rc = finish_factorization(h);
-        if (rc != UNO_KKT_OK) return rc;
-    }
-    const double* b = rhs;
-    if (!on_device) {
-        if (S.n > 0) HIPCHK(h, hipMemcpyAsync(h->bvec.p, rhs, S.n * sizeof(double), hipMemcpyHostToDevice, s));
-        b = h->bvec.p;
-    }
     const bool df = h->world == 1 && h->df_enabled && h->df_grid > 0;
     SolveArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
@@ -1427,7 +1426,6 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         TimerScope t(h, KC_SOLVE_BWD);
         HIPCHK(h, run(P0, P0.sol[q], false));
     }
-    double* xd = on_device ? x : h->bvec.p;
     {
         TimerScope t(h, KC_RHS);
         if (df) HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, S.n, s));
@@ -1456,8 +1454,47 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         if (dataflow_aborted(h)) {
             HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: redone level by level\n");
-            return uno_kkt_solve(h, rhs, x, on_device);
+            return solve_core(h, b, xd);
         }
+    }
+    return UNO_KKT_OK;
+}
+}  // namespace
+
+extern "C" {
+
+int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
+    if (!h || !rhs || !x) return UNO_KKT_ERR_ARG;
+    if (!h->analyzed || (!h->factored && !h->factor_enqueued))
+        return set_err(h, UNO_KKT_ERR_STATE, "solve before factorize");
+    HIPCHK(h, hipSetDevice(h->device));
+    Symbolic& S = h->S;
+    hipStream_t s = h->stream;
+    if (h->factor_enqueued) {  // the factorization is final only once checked (delays, null threshold)
+        int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK) return rc;
+    }
+    // iterative refinement when the last factorization accepted pivots below the threshold u (threshold
+    // relaxation instead of delayed pivots, option delay_relaxed = 0): r = A x - b with the analysed COO
+    // values (uno_kkt_symv), x -= A^-1 r
+    const int refine = (h->world == 1 && h->st.pivots_relaxed > 0 && h->values_ptr) ? h->refine : 0;
+    const double* b = rhs;
+    double* xd = x;
+    if (!on_device) {
+        if (S.n > 0) HIPCHK(h, hipMemcpyAsync(h->bvec.p, rhs, S.n * sizeof(double), hipMemcpyHostToDevice, s));
+        b = h->bvec.p;
+        xd = h->xtmp.p;
+    } else if (refine > 0 && rhs == x) {  // keep the right-hand side for the residuals
+        if (S.n > 0) HIPCHK(h, hipMemcpyAsync(h->bvec.p, rhs, S.n * sizeof(double), hipMemcpyDeviceToDevice, s));
+        b = h->bvec.p;
+    }
+    int rc = solve_core(h, b, xd);
+    if (rc != UNO_KKT_OK) return rc;
+    for (int it = 0; it < refine; ++it) {
+        HIPCHK(h, launch_neg(b, h->rtmp.p, S.n, s));              // r = -b
+        if ((rc = symv_impl(h, xd, h->rtmp.p, nullptr, nullptr)) != UNO_KKT_OK) return rc;  // r += A x
+        if ((rc = solve_core(h, h->rtmp.p, h->rtmp.p)) != UNO_KKT_OK) return rc;          // d = A^-1 r
+        HIPCHK(h, launch_sub(xd, h->rtmp.p, S.n, s));             // x -= d
     }
     h->st.solves++;
     if (!on_device) {
@@ -1624,7 +1661,10 @@ int uno_kkt_assemble_direction(uno_kkt_t h, int64_t n_vars, int64_t n_cons, cons
     return UNO_KKT_OK;
 }
 
-static int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* dot) {
+}  // extern "C"
+
+namespace {
+int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* dot) {
     if (!h->analyzed || !h->values_ptr) return set_err(h, UNO_KKT_ERR_STATE, "symv needs analysed pattern and values");
     if (h->world > 1) return set_err(h, UNO_KKT_ERR_STATE, "symv on a distributed handle");
     Symbolic& S = h->S;
@@ -1656,6 +1696,10 @@ static int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, d
     }
     return UNO_KKT_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 int uno_kkt_symv(uno_kkt_t h, const double* x, double* y) {
     if (!h || !x || !y) return UNO_KKT_ERR_ARG;

@@ -2379,6 +2379,23 @@ hipError_t launch_scatter(const double* src, const int32_t* idx, double* dst, in
     return hipGetLastError();
 }
 
+__global__ void k_neg(const double* __restrict__ b, double* __restrict__ r, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) r[i] = -b[i];
+}
+__global__ void k_sub(double* __restrict__ x, const double* __restrict__ d, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] -= d[i];
+}
+hipError_t launch_neg(const double* b, double* r, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_neg, dim3(grid_for(n, 256)), dim3(256), 0, s, b, r, n);
+    return hipGetLastError();
+}
+hipError_t launch_sub(double* x, const double* d, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_sub, dim3(grid_for(n, 256)), dim3(256), 0, s, x, d, n);
+    return hipGetLastError();
+}
+
 hipError_t launch_scatter64(const double* src, const int64_t* idx, double* dst, int64_t k, hipStream_t s) {
     if (k <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_scatter64, dim3(grid_for(k, 256)), dim3(256), 0, s, src, idx, dst, k);

@@ -164,6 +164,8 @@ hipError_t launch_normmax(const double* rowsum, const int32_t* list, int64_t n, 
 hipError_t launch_scatter(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s);  // dst[idx[t]] = src[t]
 hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int64_t k, hipStream_t s);   // dst[t] = src[idx[t]]
 hipError_t launch_scatter64(const double* src, const int64_t* idx, double* dst, int64_t k, hipStream_t s);  // dst[idx[t]] = src[t]
+hipError_t launch_neg(const double* b, double* r, int64_t n, hipStream_t s);  // r = -b
+hipError_t launch_sub(double* x, const double* d, int64_t n, hipStream_t s);   // x -= d
 size_t factor_lds_bytes(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 // one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of
