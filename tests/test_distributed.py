@@ -149,3 +149,26 @@ def test_distributed_delayed_pivots(ua):
         checked += 1
     assert checked >= 5
     assert merged > 0  # the delayed-pivot rounds were exercised
+
+
+@pytest.mark.gpu
+@pytest.mark.slow
+def test_c5_eight_ranks(ua):
+    """BASELINE.json configs[4] exactly: the C5 arrowband KKT (n = 4e6, nnz = 8e7, seed 0x5EED0005) split
+    into subtrees over 8 ranks (here 8 in-process ranks on one GPU: the same orchestration as RCCL, with
+    device-to-device copies) must give the single-GPU inertia on every rank and, on rank 0, a solution
+    bit-identical to the single-GPU one (per-front arithmetic is shared; scaling maxima are exact)."""
+    n, nv, m, r, c, v, b = ua.arrowband(4_000_000, ua.SEEDS["C5"])
+    assert len(v) > 7.9e7
+    single = ua.HipKKT(0)
+    single.analyze(n, r, c)
+    single.factorize(v)
+    ine = single.inertia()
+    xs = single.solve(b)
+    assert rel_residual(ua, n, r, c, v, xs, b) < RES_TOL
+    single.close()
+    out = run_group(ua, 8, n, r, c, (v,), b)
+    assert out[0][1]["world"] == 8 and out[0][1]["subtrees"] >= 8
+    for q in range(8):
+        assert out[q][0][0][0] == ine, q
+    np.testing.assert_array_equal(out[0][0][0][1], xs)

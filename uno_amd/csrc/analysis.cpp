@@ -432,6 +432,9 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
                 if (a != c) S.rslot[rf[std::max(a, c)]++] = (int32_t)q;
             }
         }
+        // row-major symmetric layout (kkt_kernels.hip k_rowscanR): row i = its column part, then its row
+        // part, at [cptr[i] + rptr[i], ...); the partner's original id per entry (filled below)
+        S.rowpartner.assign((size_t)(S.cptr[n] + S.rptr[n]), 0);
         for (int64_t u = 0; u < nu; ++u) {
             int32_t s = slot_of[u], b = ublk[u];
             int32_t a = S.iperm[P.ur[u]], c = S.iperm[P.uc[u]];
@@ -446,6 +449,11 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
             const uint32_t flip = S.perm[lo] > S.perm[hi] ? 0x8000u : 0u;
             S.ent_lpos[s] = ((uint32_t)lr << 16) | flip | (uint32_t)lc;
             if (!S.identity_dups) S.dup_ptr[s + 1] = P.udp[u + 1] - P.udp[u];
+        }
+        for (int64_t i = 0; i < n; ++i) {
+            int64_t t = (int64_t)S.cptr[i] + S.rptr[i];
+            for (int32_t q = S.cptr[i]; q < S.cptr[i + 1]; ++q) S.rowpartner[t++] = S.ent_r[q];
+            for (int32_t r = S.rptr[i]; r < S.rptr[i + 1]; ++r) S.rowpartner[t++] = S.ent_c[S.rslot[r]];
         }
         if (S.identity_dups) {
             for (int64_t u = 0; u < nu; ++u) S.dup_pos[slot_of[u]] = P.pos_sorted[P.udp[u]];

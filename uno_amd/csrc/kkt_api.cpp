@@ -140,7 +140,8 @@ struct uno_kkt {
     DBuf<unsigned long long> anorm, counters, stamps, fcnt, minbits;
     DBuf<double> fmin;
     int want_stamps = 0;
-    DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed;
+    DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed, rowpartner;
+    DBuf<double> uvalR;  // row-major copy of |A| (single-GPU equilibration)
     int32_t n_long = 0;
     int64_t max_long = 0, long_chunks = 0;
     DBuf<double> long_part;  // chunk results of the long-row scans
@@ -920,6 +921,10 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->cptr.upload(S.cptr, s));
     HIPCHK(h, h->rptr.upload(S.rptr, s));
     HIPCHK(h, h->rslot.upload(S.rslot, s));
+    if (h->world == 1) {
+        HIPCHK(h, h->rowpartner.upload(S.rowpartner, s));
+        HIPCHK(h, h->uvalR.alloc(S.rowpartner.size()));
+    }
     HIPCHK(h, h->fparent.upload(S.f_parent, s));
     {
         std::vector<int32_t> lr;
@@ -1016,6 +1021,8 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.rslot = h->rslot.p; SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p;
         SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p;
         SA.n_long = h->n_long; SA.max_long = h->max_long; SA.long_chunks = h->long_chunks; SA.part = h->long_part.p;
+        SA.uvalR = h->uvalR.p; SA.rowpartner = h->rowpartner.p; SA.scale_in = nullptr;
+        SA.scale_out = h->rmax.p;  // scratch of the double-buffered sweeps
         if (h->world == 1 && h->overlap_norm && !h->exact_next) {
             HIPCHK(h, launch_scale_sweeps(SA, h->scale_iters, h->rmax.p, s));
             HIPCHK(h, hipEventRecord(h->ev_scale, s));

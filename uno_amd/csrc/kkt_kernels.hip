@@ -155,6 +155,111 @@ __global__ void k_rowscan_long_fin(ScanArgs A) {
     A.out[A.perm[i]] = acc;
 }
 
+// ---- single-GPU equilibration on a row-major copy of |A| ----
+// Row i (new numbering) of the symmetric matrix = its column part (slots cptr[i] .. cptr[i+1]) followed by
+// its row part (slots rslot[rptr[i] .. rptr[i+1]]); the copy uvalR keeps |a| in that order at rows
+// [cptr[i] + rptr[i], cptr[i+1] + rptr[i+1]), with the partner's original id in rowpartner (static).
+// MODE 0 (first sweep) gathers the packed values once, writes the copy and r_i = max_j |a_ij|;
+// MODE 1 (later sweeps) and MODE 2 (row sums for ||A_pre||_inf) stream the copy.  A sweep writes the new
+// scaling into another buffer than the one it reads (double buffering), so no separate update kernel
+// is needed: s_out = s_in / sqrt(r) (s_in = 1 in the first sweep), the oracle's update.
+template <int MODE>
+__device__ __forceinline__ double rowR_finish(double acc, double si) {
+    return MODE == 2 ? acc : (acc > 0.0 ? si / sqrt(acc) : si);
+}
+
+template <int MODE>
+__global__ void k_rowscanR(ScanArgs A) {
+    constexpr int LPR = MODE == 2 ? 16 : 8;
+    const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
+    const int lane = threadIdx.x & (LPR - 1);
+    if (g >= A.n) return;
+    const int32_t i = (int32_t)g;
+    const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0;
+    const int32_t r0 = A.rptr[i], len = nc + (A.rptr[i + 1] - r0);
+    if (len > kLongRow) return;  // k_rowscanR_long
+    const int32_t orig = A.perm[i];
+    const double si = MODE == 0 ? 1.0 : (MODE == 1 ? A.scale_in[orig] : A.scale[orig]);
+    const double* sc = MODE == 1 ? A.scale_in : A.scale;
+    const int64_t base = (int64_t)c0 + r0;
+    double acc = 0.0;
+    for (int32_t t = lane; t < len; t += LPR) {
+        double w;
+        if (MODE == 0) {
+            const int32_t q = t < nc ? c0 + t : A.rslot[r0 + (t - nc)];
+            w = fabs(A.uval[q]);
+            A.uvalR[base + t] = w;
+        } else {
+            w = scaled_abs(orig, si, A.rowpartner[base + t], A.uvalR[base + t], sc);
+        }
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) {
+        const double o = __shfl_xor(acc, off);
+        acc = MODE == 2 ? acc + o : fmax(acc, o);
+    }
+    if (lane == 0) {
+        if (MODE == 2) A.out[orig] = acc;
+        else A.scale_out[orig] = rowR_finish<MODE>(acc, si);
+    }
+}
+
+// long rows: one workgroup per kLongChunk entries of the row's copy, results in chunk order
+template <int MODE>
+__global__ void k_rowscanR_long(ScanArgs A) {
+    __shared__ double red[kThreads / 64];
+    const int32_t i = A.long_rows[blockIdx.y];
+    const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0;
+    const int32_t r0 = A.rptr[i], len = nc + (A.rptr[i + 1] - r0);
+    const int64_t begin = (int64_t)blockIdx.x * kLongChunk;
+    if (begin >= len) return;
+    const int64_t end = begin + kLongChunk < len ? begin + kLongChunk : len;
+    const int32_t orig = A.perm[i];
+    const double si = MODE == 0 ? 1.0 : (MODE == 1 ? A.scale_in[orig] : A.scale[orig]);
+    const double* sc = MODE == 1 ? A.scale_in : A.scale;
+    const int64_t base = (int64_t)c0 + r0;
+    double acc = 0.0;
+    for (int64_t t = begin + threadIdx.x; t < end; t += kThreads) {
+        double w;
+        if (MODE == 0) {
+            const int32_t q = t < nc ? c0 + (int32_t)t : A.rslot[r0 + (int32_t)(t - nc)];
+            w = fabs(A.uval[q]);
+            A.uvalR[base + t] = w;
+        } else {
+            w = scaled_abs(orig, si, A.rowpartner[base + t], A.uvalR[base + t], sc);
+        }
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const double o = __shfl_xor(acc, off);
+        acc = MODE == 2 ? acc + o : fmax(acc, o);
+    }
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kThreads / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
+        A.part[(int64_t)blockIdx.y * A.long_chunks + blockIdx.x] = acc;
+    }
+}
+
+template <int MODE>
+__global__ void k_rowscanR_long_fin(ScanArgs A) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= A.n_long) return;
+    const int32_t i = A.long_rows[r];
+    const int64_t len = (A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]);
+    const int64_t nch = (len + kLongChunk - 1) / kLongChunk;
+    double acc = 0.0;
+    for (int64_t c = 0; c < nch; ++c) {
+        const double w = A.part[(int64_t)r * A.long_chunks + c];
+        acc = MODE == 2 ? acc + w : fmax(acc, w);
+    }
+    const int32_t orig = A.perm[i];
+    if (MODE == 2) A.out[orig] = acc;
+    else A.scale_out[orig] = rowR_finish<MODE>(acc, MODE == 0 ? 1.0 : A.scale_in[orig]);
+}
+
 // Partial row scans of the separator ("top") rows on one rank of a distributed factorization: the
 // rank's own slots of each top row, cut into chunks (one workgroup each, results in A.part), combined
 // per row in chunk order by k_rowscan_part_fin; the ranks' partials are then all-reduced (max / sum)
@@ -197,6 +302,10 @@ __global__ void k_scatter(const double* __restrict__ src, const int32_t* __restr
                           int64_t k) {
     for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < k; t += (int64_t)gridDim.x * blockDim.x)
         dst[idx[t]] = src[t];
+}
+
+__global__ void k_fill_ones(double* __restrict__ x, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) x[i] = 1.0;
 }
 
 __global__ void k_scatter64(const double* __restrict__ src, const int64_t* __restrict__ idx, double* __restrict__ dst,
@@ -2408,17 +2517,38 @@ hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int
     return hipGetLastError();
 }
 
+template <int MODE>
+static hipError_t launch_rowscanR(const ScanArgs& A, hipStream_t s) {
+    const int64_t threads = A.n * (MODE == 2 ? 16 : 8);
+    hipLaunchKernelGGL(k_rowscanR<MODE>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A);
+    if (A.n_long > 0) {
+        hipLaunchKernelGGL(k_rowscanR_long<MODE>, dim3((unsigned)A.long_chunks, A.n_long), dim3(kThreads), 0, s, A);
+        hipLaunchKernelGGL(k_rowscanR_long_fin<MODE>, dim3((unsigned)((A.n_long + 63) / 64)), dim3(64), 0, s, A);
+    }
+    return hipGetLastError();
+}
+
+// iters sweeps; A.scale receives the final scaling, A.scale_out (scratch, n doubles) double-buffers it
 hipError_t launch_scale_sweeps(ScanArgs A, int iters, double* rmax, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
-    for (int it = 0; it < iters; ++it) {
-        A.out = rmax;
-        hipError_t e = launch_rowscan(A, it == 0 ? 0 : 1, s);
+    (void)rmax;
+    double* final_s = A.scale;
+    double* tmp = A.scale_out;
+    if (iters == 0) {  // no scaling: s = 1 (the copy of |A| is still made for the row sums)
+        A.scale_out = tmp;
+        hipError_t e = launch_rowscanR<0>(A, s);
         if (e != hipSuccess) return e;
-        if ((e = launch_scale_update(rmax, A.scale, nullptr, A.n, it == 0 ? 1 : 0, s)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_fill_ones, dim3(grid_for(A.n, 256)), dim3(256), 0, s, final_s, A.n);
+        return hipGetLastError();
     }
-    if (iters == 0) {  // no scaling: s = 1
-        hipMemsetAsync(rmax, 0, sizeof(double) * A.n, s);
-        launch_scale_update(rmax, A.scale, nullptr, A.n, 1, s);
+    const double* in = nullptr;
+    for (int it = 0; it < iters; ++it) {
+        double* out = ((iters - 1 - it) % 2 == 0) ? final_s : tmp;  // the last sweep writes A.scale
+        A.scale_in = in;
+        A.scale_out = out;
+        hipError_t e = it == 0 ? launch_rowscanR<0>(A, s) : launch_rowscanR<1>(A, s);
+        if (e != hipSuccess) return e;
+        in = out;
     }
     return hipGetLastError();
 }
@@ -2426,7 +2556,7 @@ hipError_t launch_scale_sweeps(ScanArgs A, int iters, double* rmax, hipStream_t 
 hipError_t launch_rowsum_norm(ScanArgs A, double* rowsum, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     A.out = rowsum;
-    hipError_t e = launch_rowscan(A, 2, s);
+    hipError_t e = launch_rowscanR<2>(A, s);
     if (e != hipSuccess) return e;
     return launch_normmax(rowsum, nullptr, A.n, A.anorm, s);
 }

@@ -127,6 +127,11 @@ struct ScanArgs {
     int64_t max_long;          // longest row length among long_rows
     int64_t long_chunks;       // chunks of the longest long row (row stride of part)
     double* part;              // n_long * long_chunks chunk results (combined in chunk order)
+    // single GPU: row-major copy of |A| (k_rowscanR), double-buffered scaling sweeps
+    double* uvalR;             // cptr[n] + rptr[n] entries, row i at [cptr[i] + rptr[i], cptr[i+1] + rptr[i+1])
+    const int32_t* rowpartner; // same layout: original id of the other index of the entry
+    const double* scale_in;    // scaling read by a sweep (nullptr in the first)
+    double* scale_out;         // scaling written by a sweep (scratch n doubles on entry to launch_scale_sweeps)
 };
 constexpr int kLongRow = 2048;
 
