@@ -613,6 +613,13 @@ int oracle_kkt_inertia(oracle_kkt_t h, int64_t* pos, int64_t* neg, int64_t* zero
     return 0;
 }
 
+int oracle_kkt_scaling(oracle_kkt_t h, double* scale, double* thres) {
+    if (!h->factored) return fail(h, "scaling before factorize");
+    memcpy(scale, h->scale, sizeof(double) * (size_t)h->n);
+    *thres = h->thres;
+    return 0;
+}
+
 int oracle_kkt_stats(oracle_kkt_t h, double* out7) {
     memcpy(out7, h->stats, sizeof(h->stats));
     return 0;

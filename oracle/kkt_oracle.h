@@ -47,6 +47,8 @@ int oracle_kkt_solve(oracle_kkt_t h, const double* rhs, double* x);
 /* counters: [0] nnz_L, [1] supernodes, [2] 2x2 pivots, [3] delayed pivots, [4] null pivots,
  *           [5] factor flops, [6] max front order */
 int oracle_kkt_stats(oracle_kkt_t h, double* out7);
+/* equilibration of the last factorization: scaling by original index, null-pivot threshold */
+int oracle_kkt_scaling(oracle_kkt_t h, double* scale, double* thres);
 const char* oracle_kkt_last_error(oracle_kkt_t h);
 
 #ifdef __cplusplus

@@ -34,6 +34,7 @@ def _load():
     lib.oracle_kkt_inertia.argtypes = [ctypes.c_void_p, _i64p, _i64p, _i64p]
     lib.oracle_kkt_solve.argtypes = [ctypes.c_void_p, _f64p, _f64p]
     lib.oracle_kkt_stats.argtypes = [ctypes.c_void_p, _f64p]
+    lib.oracle_kkt_scaling.argtypes = [ctypes.c_void_p, _f64p, _f64p]
     lib.oracle_kkt_last_error.argtypes = [ctypes.c_void_p]
     lib.oracle_kkt_last_error.restype = ctypes.c_char_p
     _lib = lib
@@ -95,3 +96,14 @@ class OracleKKT:
         self.lib.oracle_kkt_stats(self.h, out.ctypes.data_as(_f64p))
         keys = ["nnz_L", "supernodes", "pivots_2x2", "delayed", "null_pivots", "flops", "max_front"]
         return dict(zip(keys, out.tolist()))
+
+
+def _scaling(self):
+    """(scale by original index, null-pivot threshold) of the last factorization."""
+    sc = np.empty(self.n)
+    th = ctypes.c_double()
+    self._check(self.lib.oracle_kkt_scaling(self.h, sc.ctypes.data_as(_f64p), ctypes.byref(th)))
+    return sc, th.value
+
+
+OracleKKT.scaling = _scaling

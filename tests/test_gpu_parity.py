@@ -42,6 +42,28 @@ def both(n, r, c, v, **opt):
     return g, o
 
 
+@pytest.mark.parametrize("case", ["c2", "random", "hub"])
+def test_scaling_bit_identical(uno_amd, case):
+    """The equilibration (ICNTL(8)=8 restated as 3 symmetric infinity-norm sweeps, MUMPSSolver.cpp:82) is
+    the oracle's to the bit: every scaling factor equal, and ||A_pre||_inf (whose summation order differs)
+    within 1e-14 relative, so the null-pivot threshold eps * 1e-5 * ||A_pre||_inf is the oracle's."""
+    from uno_amd import arrowband, SEEDS
+    from kkt_cases import null_threshold_case
+    if case == "c2":
+        n, _, _, r, c, v, _ = arrowband(10000, SEEDS["C2"])
+    elif case == "hub":  # long (chunked) rows, power-of-two scalings
+        n, r, c, v, _, _ = null_threshold_case(100_000, [2, 8], 2.0 ** 30)
+    else:
+        rr, cc, vv, _ = random_sym(np.random.default_rng(5), 60, 0.3, zero_diag_frac=0.5)
+        n, r, c, v = 60, rr, cc, vv * np.exp(np.random.default_rng(6).uniform(-20, 20, len(vv)))
+    g, o = both(n, r, c, v)
+    sg, anorm = g.debug_scaling()
+    so, thres = o.scaling()
+    assert np.isfinite(sg).all() and (sg > 0).all()
+    np.testing.assert_array_equal(sg, so)
+    assert abs(np.finfo(float).eps * 1e-5 * anorm - thres) <= 1e-14 * thres
+
+
 def test_kat_5x5(uno_amd):
     k = KATS["mumps_5x5"]
     g, o = both(k["n"], k["rows"], k["cols"], k["vals"])

@@ -174,7 +174,7 @@ std::string order_pattern(int64_t n, int64_t nnz, const int64_t* row, const int6
                           const AnalysisOptions& opt, Pattern& P) {
     P = Pattern();
     if (n < 0 || nnz < 0) return "negative size";
-    if (n >= (int64_t(1) << 31) - 1 || nnz >= (int64_t(1) << 31) - 1) return "n or nnz exceeds int32 range";
+    if (n >= (int64_t(1) << 30) || nnz >= (int64_t(1) << 31) - 1) return "n exceeds 2^30 or nnz exceeds int32 range";
     for (int64_t k = 0; k < nnz; ++k)
         if (row[k] < 0 || row[k] >= n || col[k] < 0 || col[k] >= n)
             return "COO entry " + std::to_string(k) + " out of range";
@@ -452,8 +452,10 @@ std::string build_structure(const Pattern& P, Symbolic& S) {
         }
         for (int64_t i = 0; i < n; ++i) {
             int64_t t = (int64_t)S.cptr[i] + S.rptr[i];
-            for (int32_t q = S.cptr[i]; q < S.cptr[i + 1]; ++q) S.rowpartner[t++] = S.ent_r[q];
-            for (int32_t r = S.rptr[i]; r < S.rptr[i + 1]; ++r) S.rowpartner[t++] = S.ent_c[S.rslot[r]];
+            const int32_t o = S.perm[i];
+            auto code = [&](int32_t partner) { return (S.iperm[partner] << 1) | (o > partner ? 1 : 0); };
+            for (int32_t q = S.cptr[i]; q < S.cptr[i + 1]; ++q) S.rowpartner[t++] = code(S.ent_r[q]);
+            for (int32_t r = S.rptr[i]; r < S.rptr[i + 1]; ++r) S.rowpartner[t++] = code(S.ent_c[S.rslot[r]]);
         }
         if (S.identity_dups) {
             for (int64_t u = 0; u < nu; ++u) S.dup_pos[slot_of[u]] = P.pos_sorted[P.udp[u]];

@@ -49,7 +49,7 @@ struct Symbolic {
     // column part of row i = slots [cptr[i], cptr[i+1]) (entries (r, i), r >= i, contiguous),
     // row part = rslot[rptr[i] .. rptr[i+1]) (entries (i, c), c < i)
     std::vector<int32_t> cptr, rptr, rslot;
-    std::vector<int32_t> rowpartner;   // row-major symmetric layout: partner original id (k_rowscanR)
+    std::vector<int32_t> rowpartner;   // row-major symmetric layout: (partner new index << 1) | order flag (k_rowscanR)
     // ordering (new index -> original index and inverse)
     std::vector<int32_t> perm, iperm;
     int64_t n_dense = 0;

@@ -145,6 +145,7 @@ struct uno_kkt {
     int32_t n_long = 0;
     int64_t max_long = 0, long_chunks = 0;
     DBuf<double> long_part;  // chunk results of the long-row scans
+    DBuf<uint32_t> long_cnt; // per long row: chunk arrival counter (single-GPU scans)
     unsigned long long* h_counters = nullptr;
     Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
     Plan dff_plan; // factor launches of the own fronts outside the dataflow launch (dff active)
@@ -937,6 +938,8 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, h->long_rows.upload(lr, s));
         h->long_chunks = (h->max_long + kLongChunk - 1) / kLongChunk;
         HIPCHK(h, h->long_part.alloc(std::max<int64_t>((int64_t)h->n_long * h->long_chunks, 1)));
+        HIPCHK(h, h->long_cnt.alloc(std::max<int64_t>(h->n_long, 1)));
+        HIPCHK(h, hipMemsetAsync(h->long_cnt.p, 0, sizeof(uint32_t) * std::max<int64_t>(h->n_long, 1), s));
     }
     if (h->delayed.n != (size_t)std::max<int64_t>(n, 1)) HIPCHK(h, h->delayed.alloc(std::max<int64_t>(n, 1)));
     if (h->uval.n != (size_t)S.nu) HIPCHK(h, h->uval.alloc(S.nu));
@@ -1021,8 +1024,9 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.rslot = h->rslot.p; SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p;
         SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p;
         SA.n_long = h->n_long; SA.max_long = h->max_long; SA.long_chunks = h->long_chunks; SA.part = h->long_part.p;
-        SA.uvalR = h->uvalR.p; SA.rowpartner = h->rowpartner.p; SA.scale_in = nullptr;
-        SA.scale_out = h->rmax.p;  // scratch of the double-buffered sweeps
+        SA.uvalR = h->uvalR.p; SA.rowpartner = h->rowpartner.p; SA.long_cnt = h->long_cnt.p;
+        SA.scale_out = h->rmax.p;  // scratch of the double-buffered sweeps (new numbering); final scaling after them
+        SA.scale_in = h->w.p;      // (free until the solve)
         if (h->world == 1 && h->overlap_norm && !h->exact_next) {
             HIPCHK(h, launch_scale_sweeps(SA, h->scale_iters, h->rmax.p, s));
             HIPCHK(h, hipEventRecord(h->ev_scale, s));
@@ -1601,6 +1605,21 @@ int64_t uno_kkt_debug_solve_stamps(uno_kkt_t h, uint64_t* out, int64_t cap) {
     hipStreamSynchronize(h->stream);
     hipMemcpy(out, h->df_stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost);
     return nf;
+}
+
+int uno_kkt_debug_scaling(uno_kkt_t h, double* scale, double* anorm) {
+    if (!h || !scale || !anorm) return UNO_KKT_ERR_ARG;
+    if (h->factor_enqueued) {
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
+    }
+    if (!h->factored && h->st.factorizations == 0) return set_err(h, UNO_KKT_ERR_STATE, "no factorization");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->S.n > 0) HIPCHK(h, hipMemcpy(scale, h->scale.p, sizeof(double) * h->S.n, hipMemcpyDeviceToHost));
+    unsigned long long b = 0;
+    HIPCHK(h, hipMemcpy(&b, h->anorm.p, sizeof(b), hipMemcpyDeviceToHost));
+    memcpy(anorm, &b, sizeof(b));
+    return UNO_KKT_OK;
 }
 
 const char* uno_kkt_last_error(uno_kkt_t h) { return h ? h->err.c_str() : "null handle"; }

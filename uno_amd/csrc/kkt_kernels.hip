@@ -155,111 +155,6 @@ __global__ void k_rowscan_long_fin(ScanArgs A) {
     A.out[A.perm[i]] = acc;
 }
 
-// ---- single-GPU equilibration on a row-major copy of |A| ----
-// Row i (new numbering) of the symmetric matrix = its column part (slots cptr[i] .. cptr[i+1]) followed by
-// its row part (slots rslot[rptr[i] .. rptr[i+1]]); the copy uvalR keeps |a| in that order at rows
-// [cptr[i] + rptr[i], cptr[i+1] + rptr[i+1]), with the partner's original id in rowpartner (static).
-// MODE 0 (first sweep) gathers the packed values once, writes the copy and r_i = max_j |a_ij|;
-// MODE 1 (later sweeps) and MODE 2 (row sums for ||A_pre||_inf) stream the copy.  A sweep writes the new
-// scaling into another buffer than the one it reads (double buffering), so no separate update kernel
-// is needed: s_out = s_in / sqrt(r) (s_in = 1 in the first sweep), the oracle's update.
-template <int MODE>
-__device__ __forceinline__ double rowR_finish(double acc, double si) {
-    return MODE == 2 ? acc : (acc > 0.0 ? si / sqrt(acc) : si);
-}
-
-template <int MODE>
-__global__ void k_rowscanR(ScanArgs A) {
-    constexpr int LPR = MODE == 2 ? 16 : 8;
-    const int64_t g = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) / LPR;
-    const int lane = threadIdx.x & (LPR - 1);
-    if (g >= A.n) return;
-    const int32_t i = (int32_t)g;
-    const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0;
-    const int32_t r0 = A.rptr[i], len = nc + (A.rptr[i + 1] - r0);
-    if (len > kLongRow) return;  // k_rowscanR_long
-    const int32_t orig = A.perm[i];
-    const double si = MODE == 0 ? 1.0 : (MODE == 1 ? A.scale_in[orig] : A.scale[orig]);
-    const double* sc = MODE == 1 ? A.scale_in : A.scale;
-    const int64_t base = (int64_t)c0 + r0;
-    double acc = 0.0;
-    for (int32_t t = lane; t < len; t += LPR) {
-        double w;
-        if (MODE == 0) {
-            const int32_t q = t < nc ? c0 + t : A.rslot[r0 + (t - nc)];
-            w = fabs(A.uval[q]);
-            A.uvalR[base + t] = w;
-        } else {
-            w = scaled_abs(orig, si, A.rowpartner[base + t], A.uvalR[base + t], sc);
-        }
-        acc = MODE == 2 ? acc + w : fmax(acc, w);
-    }
-#pragma unroll
-    for (int off = LPR / 2; off > 0; off >>= 1) {
-        const double o = __shfl_xor(acc, off);
-        acc = MODE == 2 ? acc + o : fmax(acc, o);
-    }
-    if (lane == 0) {
-        if (MODE == 2) A.out[orig] = acc;
-        else A.scale_out[orig] = rowR_finish<MODE>(acc, si);
-    }
-}
-
-// long rows: one workgroup per kLongChunk entries of the row's copy, results in chunk order
-template <int MODE>
-__global__ void k_rowscanR_long(ScanArgs A) {
-    __shared__ double red[kThreads / 64];
-    const int32_t i = A.long_rows[blockIdx.y];
-    const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0;
-    const int32_t r0 = A.rptr[i], len = nc + (A.rptr[i + 1] - r0);
-    const int64_t begin = (int64_t)blockIdx.x * kLongChunk;
-    if (begin >= len) return;
-    const int64_t end = begin + kLongChunk < len ? begin + kLongChunk : len;
-    const int32_t orig = A.perm[i];
-    const double si = MODE == 0 ? 1.0 : (MODE == 1 ? A.scale_in[orig] : A.scale[orig]);
-    const double* sc = MODE == 1 ? A.scale_in : A.scale;
-    const int64_t base = (int64_t)c0 + r0;
-    double acc = 0.0;
-    for (int64_t t = begin + threadIdx.x; t < end; t += kThreads) {
-        double w;
-        if (MODE == 0) {
-            const int32_t q = t < nc ? c0 + (int32_t)t : A.rslot[r0 + (int32_t)(t - nc)];
-            w = fabs(A.uval[q]);
-            A.uvalR[base + t] = w;
-        } else {
-            w = scaled_abs(orig, si, A.rowpartner[base + t], A.uvalR[base + t], sc);
-        }
-        acc = MODE == 2 ? acc + w : fmax(acc, w);
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        const double o = __shfl_xor(acc, off);
-        acc = MODE == 2 ? acc + o : fmax(acc, o);
-    }
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        for (int w = 1; w < kThreads / 64; ++w) acc = MODE == 2 ? acc + red[w] : fmax(acc, red[w]);
-        A.part[(int64_t)blockIdx.y * A.long_chunks + blockIdx.x] = acc;
-    }
-}
-
-template <int MODE>
-__global__ void k_rowscanR_long_fin(ScanArgs A) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= A.n_long) return;
-    const int32_t i = A.long_rows[r];
-    const int64_t len = (A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]);
-    const int64_t nch = (len + kLongChunk - 1) / kLongChunk;
-    double acc = 0.0;
-    for (int64_t c = 0; c < nch; ++c) {
-        const double w = A.part[(int64_t)r * A.long_chunks + c];
-        acc = MODE == 2 ? acc + w : fmax(acc, w);
-    }
-    const int32_t orig = A.perm[i];
-    if (MODE == 2) A.out[orig] = acc;
-    else A.scale_out[orig] = rowR_finish<MODE>(acc, MODE == 0 ? 1.0 : A.scale_in[orig]);
-}
-
 // Partial row scans of the separator ("top") rows on one rank of a distributed factorization: the
 // rank's own slots of each top row, cut into chunks (one workgroup each, results in A.part), combined
 // per row in chunk order by k_rowscan_part_fin; the ranks' partials are then all-reduced (max / sum)
@@ -395,12 +290,144 @@ __device__ __forceinline__ bool df_wait(const uint32_t* addr, uint32_t target, u
 // every store of this wave has completed (sc1 stores: written through) before the signal below
 __device__ __forceinline__ void drain_stores() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+// ---- single-GPU equilibration on a row-major copy of |A| ----
+// Row i (new numbering) of the symmetric matrix = its column part (slots cptr[i] .. cptr[i+1]) followed by
+// its row part (slots rslot[rptr[i] .. rptr[i+1]]); the copy uvalR keeps |a| in that order at
+// [cptr[i] + rptr[i], cptr[i+1] + rptr[i+1]).  rowpartner holds (partner's new index << 1) | (the row's
+// original id > the partner's), so the scalings are kept in the NEW numbering (a row's partners are its
+// nested-dissection neighbours: the gathers stay in cache) and the product is still formed in the oracle's
+// order (s of the larger original id first).  MODE 0 (first sweep) gathers the packed values once and
+// writes the copy; MODE 1 (later sweeps) and MODE 2 (row sums for ||A_pre||_inf) stream it.  A sweep reads
+// one scaling buffer and writes another (s_out = s_in / sqrt(r), s_in = 1 in the first sweep).  Rows longer
+// than kLongRow are cut into chunks handled by the first blocks of the same launch; the last chunk block
+// of a row to finish (arrival counter) combines the chunk results in chunk order (deterministic).
+template <int MODE>
+__device__ __forceinline__ double rowR_term(const ScanArgs& A, int64_t t, int32_t i, int32_t c0, int32_t nc,
+                                            int32_t r0, double si, const double* __restrict__ sc) {
+    if (MODE == 0) {
+        const int32_t q = t < nc ? c0 + (int32_t)t : A.rslot[r0 + (int32_t)(t - nc)];
+        const double w = fabs(A.uval[q]);
+        A.uvalR[(int64_t)c0 + r0 + t] = w;
+        return w;
+    }
+    const int64_t e = (int64_t)c0 + r0 + t;
+    const int32_t pc = A.rowpartner[e];
+    const double v = A.uvalR[e], sj = sc[pc >> 1];
+    return (pc & 1) ? si * v * sj : sj * v * si;  // |v| >= 0: no fabs needed
+}
+
+template <int MODE>
+__device__ __forceinline__ void rowR_write(const ScanArgs& A, int32_t i, double acc, double si) {
+    if (MODE == 2) A.out[i] = acc;
+    else A.scale_out[i] = acc > 0.0 ? si / sqrt(acc) : si;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void k_rowscanR(ScanArgs A) {
+    const double* sc = MODE == 1 ? A.scale_in : A.scale_out;  // MODE 2: the final scaling (new numbering)
+    const int64_t nlb = (int64_t)A.n_long * A.long_chunks;
+    if ((int64_t)blockIdx.x < nlb) {  // chunk of a long row
+        __shared__ double red[4];
+        __shared__ int last;
+        const int r = (int)(blockIdx.x / A.long_chunks), ch = (int)(blockIdx.x % A.long_chunks);
+        const int32_t i = A.long_rows[r];
+        const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0, r0 = A.rptr[i];
+        const int64_t len = nc + (A.rptr[i + 1] - r0);
+        const int64_t nch = (len + kLongChunk - 1) / kLongChunk;
+        if (ch >= nch) return;
+        const double si = MODE == 0 ? 1.0 : sc[i];
+        const int64_t end = (int64_t)(ch + 1) * kLongChunk < len ? (int64_t)(ch + 1) * kLongChunk : len;
+        double acc = 0.0;
+        for (int64_t t = (int64_t)ch * kLongChunk + threadIdx.x; t < end; t += 256) {
+            const double w = rowR_term<MODE>(A, t, i, c0, nc, r0, si, sc);
+            acc = MODE == 2 ? acc + w : fmax(acc, w);
+        }
+        for (int off = 32; off > 0; off >>= 1) {
+            const double o = __shfl_xor(acc, off);
+            acc = MODE == 2 ? acc + o : fmax(acc, o);
+        }
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            acc = MODE == 2 ? (red[0] + red[1]) + (red[2] + red[3]) : fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+            st_sc1(A.part + (int64_t)r * A.long_chunks + ch, acc);
+            drain_stores();
+            last = __hip_atomic_fetch_add(A.long_cnt + r, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (uint32_t)(nch - 1);
+        }
+        __syncthreads();
+        if (last && threadIdx.x == 0) {
+            double tot = 0.0;
+            for (int64_t c = 0; c < nch; ++c) {
+                const double w = ld_sc1(A.part + (int64_t)r * A.long_chunks + c);
+                tot = MODE == 2 ? tot + w : fmax(tot, w);
+            }
+            rowR_write<MODE>(A, i, tot, si);
+            __hip_atomic_store(A.long_cnt + r, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
+        }
+        return;
+    }
+    constexpr int LPR = MODE == 2 ? 16 : 8;
+    constexpr int U = 64 / LPR;  // entries per lane per batch: a row of <= 64 entries takes one batch, whose
+                                 // loads are all issued before the first use (two dependent round trips)
+    const int64_t g = ((int64_t)(blockIdx.x - nlb) * blockDim.x + threadIdx.x) / LPR;
+    const int lane = threadIdx.x & (LPR - 1);
+    if (g >= A.n) return;
+    const int32_t i = (int32_t)g;
+    const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0;
+    const int32_t r0 = A.rptr[i], len = nc + (A.rptr[i + 1] - r0);
+    if (len > kLongRow) return;  // chunk blocks above
+    const double si = MODE == 0 ? 1.0 : sc[i];
+    const int64_t e0 = (int64_t)c0 + r0;
+    double acc = 0.0;
+    for (int32_t b = 0; b < len; b += LPR * U) {
+        int32_t key[U];
+        double v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = b + lane + LPR * u;
+            const bool ok = t < len;
+            if (MODE == 0) key[u] = !ok ? c0 : (t < nc ? c0 + t : A.rslot[r0 + (t - nc)]);  // packed slot
+            else { key[u] = ok ? A.rowpartner[e0 + t] : 0; v[u] = ok ? A.uvalR[e0 + t] : 0.0; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int32_t t = b + lane + LPR * u;
+            double w;
+            if (MODE == 0) {
+                w = fabs(A.uval[key[u]]);
+                if (t < len) A.uvalR[e0 + t] = w;
+                else w = 0.0;
+            } else {
+                const double sj = sc[key[u] >> 1];
+                w = (key[u] & 1) ? si * v[u] * sj : sj * v[u] * si;  // v = 0 beyond the row
+            }
+            acc = MODE == 2 ? acc + w : fmax(acc, w);
+        }
+    }
+#pragma unroll
+    for (int off = LPR / 2; off > 0; off >>= 1) {
+        const double o = __shfl_xor(acc, off);
+        acc = MODE == 2 ? acc + o : fmax(acc, o);
+    }
+    if (lane == 0) rowR_write<MODE>(A, i, acc, si);
+}
+
+// scaling by original id for the factorization / solve kernels: scale[perm[i]] = scaleN[i]
+__global__ void k_scale_to_orig(const double* __restrict__ sn, const int32_t* __restrict__ perm, double* __restrict__ scale,
+                                int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        scale[perm[i]] = sn[i];
+}
+
 // ------------------------------------------------------------------------------------------------
 // dense front factorization
 // ------------------------------------------------------------------------------------------------
 // Front storage: only the lower triangle A(i,j), j <= i, is kept.
 //   PackedStore: row-packed lower triangle in LDS, m(m+1)/2 doubles (row i starts at i(i+1)/2)
 //   FullStore:   m x ld square (fronts too large for LDS live in HBM scratch)
+// doubles of a front's packed lower triangle in LDS, rounded up to even (16-byte alignment of what follows)
+__device__ __forceinline__ int64_t packed_even(int m) { return (((int64_t)m * (m + 1) / 2) + 1) & ~1ll; }
+
 struct PackedStore {
     double* F;
     __device__ __forceinline__ int idx(int i, int j) const { return ((i * (i + 1)) >> 1) + j; }
@@ -1231,7 +1258,6 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 
 // LDS layout of one front: [FrontShared 32 B][packed lower m(m+1)/2, even][sloc m][coefB m]
 // [lrow m][rstage/lorig m][piv m]
-__device__ __forceinline__ int64_t packed_even(int m) { return (((int64_t)m * (m + 1) / 2) + 1) & ~1ll; }
 
 template <int NT, int MR>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MR > 8 ? 2 : 3))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
@@ -2520,39 +2546,34 @@ hipError_t launch_gather(const double* src, const int32_t* idx, double* dst, int
 template <int MODE>
 static hipError_t launch_rowscanR(const ScanArgs& A, hipStream_t s) {
     const int64_t threads = A.n * (MODE == 2 ? 16 : 8);
-    hipLaunchKernelGGL(k_rowscanR<MODE>, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A);
-    if (A.n_long > 0) {
-        hipLaunchKernelGGL(k_rowscanR_long<MODE>, dim3((unsigned)A.long_chunks, A.n_long), dim3(kThreads), 0, s, A);
-        hipLaunchKernelGGL(k_rowscanR_long_fin<MODE>, dim3((unsigned)((A.n_long + 63) / 64)), dim3(64), 0, s, A);
-    }
+    const int64_t blocks = (threads + 255) / 256 + (int64_t)A.n_long * A.long_chunks;
+    hipLaunchKernelGGL(k_rowscanR<MODE>, dim3((unsigned)blocks), dim3(256), 0, s, A);
     return hipGetLastError();
 }
 
-// iters sweeps; A.scale receives the final scaling, A.scale_out (scratch, n doubles) double-buffers it
+// iters sweeps over the row-major copy.  The scalings live in the new numbering in A.scale_in / A.scale_out
+// (two scratch buffers of n doubles, the last sweep writes A.scale_out); A.scale (by original id) receives
+// the final one.
 hipError_t launch_scale_sweeps(ScanArgs A, int iters, double* rmax, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     (void)rmax;
-    double* final_s = A.scale;
-    double* tmp = A.scale_out;
-    if (iters == 0) {  // no scaling: s = 1 (the copy of |A| is still made for the row sums)
-        A.scale_out = tmp;
-        hipError_t e = launch_rowscanR<0>(A, s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_fill_ones, dim3(grid_for(A.n, 256)), dim3(256), 0, s, final_s, A.n);
-        return hipGetLastError();
-    }
-    const double* in = nullptr;
-    for (int it = 0; it < iters; ++it) {
-        double* out = ((iters - 1 - it) % 2 == 0) ? final_s : tmp;  // the last sweep writes A.scale
-        A.scale_in = in;
+    double* bufs[2] = {A.scale_out, const_cast<double*>(A.scale_in)};
+    double* out = nullptr;
+    for (int it = 0; it < (iters > 0 ? iters : 1); ++it) {
+        out = bufs[(iters - 1 - it) % 2 == 0 ? 0 : 1];  // the last sweep writes bufs[0] (the final scaling)
+        A.scale_in = it == 0 ? nullptr : (out == bufs[0] ? bufs[1] : bufs[0]);
         A.scale_out = out;
         hipError_t e = it == 0 ? launch_rowscanR<0>(A, s) : launch_rowscanR<1>(A, s);
         if (e != hipSuccess) return e;
-        in = out;
     }
+    if (iters == 0) {  // no scaling: s = 1 (the first pass above only built the copy of |A|)
+        hipLaunchKernelGGL(k_fill_ones, dim3(grid_for(A.n, 256)), dim3(256), 0, s, bufs[0], A.n);
+    }
+    hipLaunchKernelGGL(k_scale_to_orig, dim3(grid_for(A.n, 256)), dim3(256), 0, s, bufs[0], A.perm, A.scale, A.n);
     return hipGetLastError();
 }
 
+// row sums of the equilibrated matrix and ||A_pre||_inf; A.scale_out = the final scaling (new numbering)
 hipError_t launch_rowsum_norm(ScanArgs A, double* rowsum, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     A.out = rowsum;

@@ -127,11 +127,12 @@ struct ScanArgs {
     int64_t max_long;          // longest row length among long_rows
     int64_t long_chunks;       // chunks of the longest long row (row stride of part)
     double* part;              // n_long * long_chunks chunk results (combined in chunk order)
-    // single GPU: row-major copy of |A| (k_rowscanR), double-buffered scaling sweeps
+    // single GPU: row-major copy of |A| (k_rowscanR), double-buffered scaling sweeps in the new numbering
     double* uvalR;             // cptr[n] + rptr[n] entries, row i at [cptr[i] + rptr[i], cptr[i+1] + rptr[i+1])
-    const int32_t* rowpartner; // same layout: original id of the other index of the entry
-    const double* scale_in;    // scaling read by a sweep (nullptr in the first)
-    double* scale_out;         // scaling written by a sweep (scratch n doubles on entry to launch_scale_sweeps)
+    const int32_t* rowpartner; // same layout: (partner's new index << 1) | (row's original id > partner's)
+    const double* scale_in;    // launch_scale_sweeps: second scratch buffer (n); in a sweep: the scaling read
+    double* scale_out;         // launch_scale_sweeps: first scratch buffer (n), holds the final scaling after it
+    uint32_t* long_cnt;        // per long row: chunk arrival counter (zero between launches)
 };
 constexpr int kLongRow = 2048;
 

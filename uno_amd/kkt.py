@@ -97,6 +97,7 @@ def load_library():
     lib.uno_kkt_group_destroy.restype = None
     lib.uno_kkt_attach_local.argtypes = [vp, vp, ctypes.c_int]
     lib.uno_kkt_dist_info.argtypes = [vp, ctypes.POINTER(KKTDistInfo)]
+    lib.uno_kkt_debug_scaling.argtypes = [vp, _f64p, _f64p]
     lib.uno_kkt_debug_partition.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _i64p]
     lib.uno_kkt_debug_partition.restype = ctypes.c_int64
@@ -196,6 +197,13 @@ class HipKKT:
 
     def solve_device(self, rhs_ptr, x_ptr):
         self._check(self.lib.uno_kkt_solve(self.h, ctypes.c_void_p(int(rhs_ptr)), ctypes.c_void_p(int(x_ptr)), 1))
+
+    def debug_scaling(self):
+        """(scale by original index, ||A_pre||_inf) of the last factorization (uno_kkt_debug.h)."""
+        sc = np.empty(self.n)
+        an = ctypes.c_double()
+        self._check(self.lib.uno_kkt_debug_scaling(self.h, sc.ctypes.data_as(_f64p), ctypes.byref(an)))
+        return sc, an.value
 
     def stats(self):
         s = KKTStats()
