@@ -43,8 +43,10 @@ def parse():
     ap.add_argument("--n", type=int, default=0,
                     help="KKT dimension per GPU (default: 1e6 = C3 on one GPU / in replicas; 5e5 per GPU in dist mode, "
                          "C5 = 4e6 at 8 GPUs)")
-    ap.add_argument("--mode", choices=["dist", "replicas"], default="dist",
-                    help="N>1: one system partitioned over the GPUs (dist) or one system per GPU (replicas)")
+    ap.add_argument("--mode", choices=["dist", "replicas", "ipm"], default="dist",
+                    help="N>1: one system partitioned over the GPUs (dist) or one system per GPU (replicas); "
+                         "ipm: an interior-point-like sequence through the drop-in's host-value path (1 GPU)")
+    ap.add_argument("--ipm-iters", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-n", type=int, default=1_000_000)
     ap.add_argument("--profile-only", action="store_true", help="skip event pass and CPU baseline")
@@ -54,8 +56,69 @@ def parse():
     return ap.parse_args()
 
 
+def run_ipm(args):
+    """An interior-point-like sequence at C3 through the path the Uno plugin takes (integration/HIPLDLSolver.cpp):
+    values on the HOST (page-locked once), every iteration a new barrier diagonal Sigma (log-uniform in
+    [1e-8, 1e8], the late-IPM spread) uploaded in full, then the inertia-correction loop of
+    PrimalDualRegularization.hpp:133-219 (delta_w = 1e-4, then x8 / x100) whose retries upload only the
+    regularization diagonal (uno_kkt_factorize_update), then one solve with host rhs / solution.  Threshold
+    relaxation instead of delayed pivots (the plugin's setting), so no re-analysis happens inside the loop.
+    Reports the end-to-end wall time per iteration and per factorization, PCIe included."""
+    import torch
+    import uno_amd
+    uno_amd.load_library()
+    torch.cuda.init()
+    n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(args.n or 1_000_000, uno_amd.SEEDS["C3"])
+    nh = sum(min(j, 12) + 1 for j in range(nv))
+    sig0 = n + nh  # Sigma positions [sig0, sig0 + nv) (uno_amd/csrc/arrowband.c layout)
+    kkt = uno_amd.HipKKT(0, delay_relaxed=0, pin_host_values=1)
+    kkt.analyze(n, rows, cols)
+    v = np.array(vals)
+    rng = np.random.default_rng(7)
+    kkt.factorize(v)
+    kkt.inertia()
+    kkt.solve(rhs)
+    torch.cuda.synchronize()
+    its, facs, retries, t_it = [], 0, 0, []
+    for it in range(args.ipm_iters):
+        v[sig0:sig0 + nv] = 10.0 ** rng.uniform(-8, 8, nv)
+        v[:n] = 0.0
+        t0 = time.perf_counter()
+        kkt.factorize(v)
+        inertia = kkt.inertia()
+        nf, dw = 1, 0.0
+        while inertia != (nv, m, 0) and nf < 12:
+            dw = 1e-4 if dw == 0.0 else dw * (100.0 if nf > 8 else 8.0)
+            v[:nv] = dw
+            v[nv:n] = -1e-8
+            kkt.factorize_update(v, 0, n)
+            inertia = kkt.inertia()
+            nf += 1
+        x = kkt.solve(rhs)
+        t_it.append(time.perf_counter() - t0)
+        facs += nf
+        retries += nf - 1
+        its.append(list(inertia))
+    st = kkt.stats()
+    res = np.abs(uno_amd.coo_symv(n, rows, cols, v, x) - rhs).max()
+    absk = uno_amd.coo_symv(n, rows, cols, np.abs(v), np.ones(n)).max()
+    total = sum(t_it)
+    print(json.dumps({
+        "metric": "KKT factorizations/s, IPM-like sequence through the drop-in host-value path (C3, PCIe included)",
+        "value": round(facs / total, 3), "unit": "factorizations/s", "n_gpus": 1, "higher_is_better": True,
+        "iterations": args.ipm_iters, "factorizations": facs, "inertia_correction_retries": retries,
+        "ms_per_iteration_median": round(1e3 * float(np.median(t_it)), 3), "ms_per_factorization": round(1e3 * total / facs, 3),
+        "fronts_merged": st["fronts_merged"], "pivots_relaxed_last": st["pivots_relaxed"],
+        "rel_residual_last": float(res / (absk * np.abs(x).max() + np.abs(rhs).max())),
+        "config": {"workload": "C3 arrowband KKT, Sigma redrawn per iteration, delta_w retries, host values + rhs",
+                   "n": n, "nnz": len(vals), "full_upload_bytes": 8 * len(vals), "retry_upload_bytes": 8 * n},
+    }))
+
+
 def main():
     args = parse()
+    if args.mode == "ipm":
+        return run_ipm(args)
     import torch
     import torch.distributed as dist
 

@@ -83,6 +83,14 @@ int uno_kkt_analyze(uno_kkt_t handle, int64_t n, int64_t nnz, const int64_t* row
  * Replaces do_numerical_factorization / JOB=2 (MUMPSSolver.cpp:85-89). */
 int uno_kkt_factorize(uno_kkt_t handle, const double* values, int values_on_device);
 
+/* Refactorization after a host-side edit of positions [first, first + count) only: `values` is the whole
+ * host COO array of the previous host-pointer factorization, of which only that range is copied.  The
+ * inertia-correction loop (PrimalDualRegularization.hpp:178-179, 210-211) rewrites only the regularization
+ * diagonal, which COOFormat stores first (COOFormat.hpp:102-110), so each retry moves reg_size doubles
+ * instead of nnz.  Options: "pin_host_values" (1: the host buffer is page-locked once with hipHostRegister,
+ * so uploads are direct DMA; it must stay allocated while the handle uses it). */
+int uno_kkt_factorize_update(uno_kkt_t handle, const double* values, int64_t first, int64_t count);
+
 /* Device-side value edits between factorizations (the inertia-correction loop changes only the
  * regularization diagonal: COOFormat::set_regularization, COOFormat.hpp:102-110). */
 int uno_kkt_set_values(uno_kkt_t handle, const int64_t* positions, const double* values, int64_t count);

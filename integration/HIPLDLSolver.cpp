@@ -23,6 +23,8 @@ namespace uno {
          // iterative refinement (option "refine").  UNO_KKT_OPTIONS=delay_relaxed=1 restores the delays.
          const char* env = std::getenv("UNO_KKT_OPTIONS");
          if (env == nullptr || std::strstr(env, "delay_relaxed") == nullptr) uno_kkt_set_option(h, "delay_relaxed", 0.0);
+         // the plugin owns its COO storage (MUMPSSolver.hpp:52): page-lock it once for direct uploads
+         uno_kkt_set_option(h, "pin_host_values", 1.0);
          return h;
       }
       void hip_destroy(void* h) { uno_kkt_destroy(static_cast<uno_kkt_t>(h)); }
@@ -30,6 +32,9 @@ namespace uno {
          return uno_kkt_analyze(static_cast<uno_kkt_t>(h), n, nnz, r, c);
       }
       int hip_factorize(void* h, const double* v) { return uno_kkt_factorize(static_cast<uno_kkt_t>(h), v, 0); }
+      int hip_factorize_update(void* h, const double* v, int64_t first, int64_t count) {
+         return uno_kkt_factorize_update(static_cast<uno_kkt_t>(h), v, first, count);
+      }
       int hip_inertia(void* h, int64_t* p, int64_t* q, int64_t* z) {
          return uno_kkt_inertia(static_cast<uno_kkt_t>(h), p, q, z);
       }
@@ -38,8 +43,8 @@ namespace uno {
    } // namespace
 
    const KKTBackend& hip_kkt_backend() {
-      static const KKTBackend backend{"HIPLDL", hip_create, hip_destroy, hip_analyze, hip_factorize, hip_inertia, hip_solve,
-         hip_last_error};
+      static const KKTBackend backend{"HIPLDL", hip_create, hip_destroy, hip_analyze, hip_factorize, hip_factorize_update,
+         hip_inertia, hip_solve, hip_last_error};
       return backend;
    }
 
@@ -68,6 +73,7 @@ namespace uno {
    void HIPLDLSolver::initialize_memory(size_t number_variables, size_t number_constraints, size_t number_hessian_nonzeros,
          size_t regularization_size) {
       this->dimension = number_variables + number_constraints;
+      this->regularization_size = regularization_size;
       const size_t number_nonzeros = number_hessian_nonzeros + regularization_size;
       this->row_indices.reserve(number_nonzeros);
       this->column_indices.reserve(number_nonzeros);
@@ -99,7 +105,17 @@ namespace uno {
       if (matrix.number_nonzeros() != this->analysed_nonzeros) {
          throw std::runtime_error("HIPLDL: the pattern changed since the symbolic analysis");
       }
-      this->check(this->backend.factorize(this->handle, matrix.data_pointer()), "factorize");
+      // inertia-correction retry: only the regularization diagonal (positions [0, reg_size)) changed
+      const bool retry = this->in_regularization && !this->values_fresh && this->backend.factorize_update != nullptr &&
+         matrix.data_pointer() == this->augmented_matrix.data_pointer();
+      if (retry) {
+         this->check(this->backend.factorize_update(this->handle, matrix.data_pointer(), 0,
+            static_cast<int64_t>(this->regularization_size)), "factorize");
+      }
+      else {
+         this->check(this->backend.factorize(this->handle, matrix.data_pointer()), "factorize");
+      }
+      this->values_fresh = false;
       this->check(this->backend.inertia(this->handle, &this->positive, &this->negative, &this->zero), "inertia");
       kkt_trace::record_factorization(this->dimension, this->positive, this->negative, this->zero);
    }
@@ -125,6 +141,12 @@ namespace uno {
       if (warmstart_information.objective_changed || warmstart_information.constraints_changed) {
          this->augmented_matrix.reset();
          subproblem.assemble_augmented_matrix(statistics, this->augmented_matrix, this->constraint_jacobian);
+         this->values_fresh = true;
+         struct Scope {  // also reset when the loop throws (UnstableRegularization, FeasibilityRestoration.cpp:103-105)
+            bool& flag;
+            explicit Scope(bool& f): flag(f) { flag = true; }
+            ~Scope() { flag = false; }
+         } scope(this->in_regularization);
          subproblem.regularize_augmented_matrix(statistics, this->augmented_matrix, subproblem.dual_regularization_factor(), *this);
          subproblem.assemble_augmented_rhs(this->objective_gradient, this->constraints, this->constraint_jacobian, this->rhs);
       }

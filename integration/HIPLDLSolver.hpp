@@ -29,6 +29,8 @@ namespace uno {
       void (*destroy)(void* handle);
       int (*analyze)(void* handle, int64_t n, int64_t nnz, const int64_t* row, const int64_t* col);
       int (*factorize)(void* handle, const double* values);
+      // refactorization after an edit of positions [first, first + count) of the same host array
+      int (*factorize_update)(void* handle, const double* values, int64_t first, int64_t count);
       int (*inertia)(void* handle, int64_t* positive, int64_t* negative, int64_t* zero);
       int (*solve)(void* handle, const double* rhs, double* x);
       const char* (*last_error)(void* handle);
@@ -61,6 +63,12 @@ namespace uno {
       void* handle{nullptr};
       size_t dimension{0};
       size_t analysed_nonzeros{0};
+      size_t regularization_size{0};
+      // inside the adapter's orchestration (solve_indefinite_system below), between the assembly and the
+      // right-hand side: the first factorization uploads every value, the inertia-correction retries only
+      // the regularization diagonal, which COOFormat stores first (COOFormat.hpp:102-110)
+      bool in_regularization{false};
+      bool values_fresh{true};
       // inertia of the last factorization, cached (one device sync per factorization)
       int64_t positive{0}, negative{0}, zero{0};
 

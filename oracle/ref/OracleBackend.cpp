@@ -19,7 +19,7 @@ namespace uno {
       int o_solve(void* h, const double* b, double* x) { return oracle_kkt_solve(static_cast<oracle_kkt_t>(h), b, x); }
       const char* o_last_error(void* h) { return oracle_kkt_last_error(static_cast<oracle_kkt_t>(h)); }
       const KKTBackend& oracle_backend() {
-         static const KKTBackend b{"ORACLE", o_create, o_destroy, o_analyze, o_factorize, o_inertia, o_solve, o_last_error};
+         static const KKTBackend b{"ORACLE", o_create, o_destroy, o_analyze, o_factorize, nullptr, o_inertia, o_solve, o_last_error};
          return b;
       }
    } // namespace

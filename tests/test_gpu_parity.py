@@ -304,3 +304,30 @@ def test_threshold_relaxation_with_refinement(uno_amd):
     g.solve_device(bd.data_ptr(), bd.data_ptr())
     torch.cuda.synchronize()
     np.testing.assert_allclose(bd.cpu().numpy(), xg, rtol=1e-12, atol=1e-14 * np.abs(xg).max())
+
+
+def test_factorize_update_prefix(uno_amd):
+    """uno_kkt_factorize_update (the plugin's inertia-correction retries): after a host-pointer
+    factorization, uploading only positions [0, n) (the regularization diagonal Uno stores first,
+    COOFormat.hpp:102-110) gives the factorization of the edited array: same inertia and solution as a
+    full upload and as the oracle; page-locked host values (pin_host_values) give the same results."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(20000, SEEDS["C2"])
+    g = HipKKT(0, pin_host_values=1)
+    full = HipKKT(0)
+    g.analyze(n, r, c)
+    full.analyze(n, r, c)
+    o = OracleKKT()
+    o.analyze(n, r, c)
+    vals = v.copy()
+    g.factorize(vals)
+    for dw in (1e-4, 8e-4, 6.4e-3, 1.0):
+        vals[:nv] = dw
+        vals[nv:n] = -1e-8
+        g.factorize_update(vals, 0, n)
+        full.factorize(vals.copy())
+        o.factorize(vals)
+        assert g.inertia() == full.inertia() == o.inertia()
+        np.testing.assert_array_equal(g.solve(b), full.solve(b))
+    with pytest.raises(RuntimeError):
+        g.factorize_update(vals, n - 1, len(vals))  # range beyond the array

@@ -183,6 +183,8 @@ struct uno_kkt {
     DBuf<double> symv_tmp, symv_part, dot_d;
     DBuf<double> xtmp, rtmp;              // host-pointer solves / refinement residuals
     int refine = 1;                       // refinement steps after a factorization with relaxed pivots
+    int pin_host = 0;                     // option pin_host_values
+    const double* pinned_ptr = nullptr;   // caller buffer registered with hipHostRegister
     DBuf<int64_t> edit_pos;               // uno_kkt_set_values staging
     DBuf<double> edit_val;
     bool packed_valid = false;            // uval holds the current values (symv reuses the factor's pack)
@@ -1189,6 +1191,7 @@ void uno_kkt_destroy(uno_kkt_t h) {
     for (auto e : h->ev_pool) hipEventDestroy(e);
     if (h->h_counters) hipHostFree(h->h_counters);
     if (h->h_big) hipHostFree(h->h_big);
+    if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
     if (h->stream2) hipStreamSynchronize(h->stream2);
     if (h->ev_scale) hipEventDestroy(h->ev_scale);
     if (h->ev_norm) hipEventDestroy(h->ev_norm);
@@ -1213,6 +1216,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "timing") h->timing = value != 0.0;
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
     else if (n == "refine") h->refine = std::max(0, (int)value);
+    else if (n == "pin_host_values") h->pin_host = value != 0.0;
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else if (n == "gather_solution") h->gather_solution = value != 0.0;
@@ -1253,6 +1257,7 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
     h->analyzed = h->factored = h->factor_enqueued = false;
     h->values_ptr = nullptr;
     h->merges_total = 0;
+    if (h->pinned_ptr) { hipHostUnregister(const_cast<double*>(h->pinned_ptr)); h->pinned_ptr = nullptr; }
     auto t0 = std::chrono::steady_clock::now();
     std::string msg = ukkt::analyze(n, nnz, row, col, h->aopt, h->P, h->S);
     if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
@@ -1318,6 +1323,21 @@ int uno_kkt_fill_values(uno_kkt_t h, int64_t first, int64_t count, double value)
     return UNO_KKT_OK;
 }
 
+int uno_kkt_factorize_update(uno_kkt_t h, const double* values, int64_t first, int64_t count) {
+    if (!h || !values) return UNO_KKT_ERR_ARG;
+    if (!h->analyzed) return set_err(h, UNO_KKT_ERR_STATE, "factorize before analyze");
+    if (h->values_ptr != h->values.p) return set_err(h, UNO_KKT_ERR_STATE, "factorize_update needs a previous host-pointer factorization");
+    if (first < 0 || count < 0 || first + count > h->S.nnz) return set_err(h, UNO_KKT_ERR_ARG, "range out of bounds");
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->factor_enqueued) {  // its redos re-pack from the device copy: finish it before the copy changes
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
+    }
+    if (count > 0)
+        HIPCHK(h, hipMemcpyAsync(h->values.p + first, values + first, count * sizeof(double), hipMemcpyHostToDevice, h->stream));
+    return uno_kkt_factorize(h, nullptr, 0);
+}
+
 int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     if (!h) return UNO_KKT_ERR_ARG;
     if (!h->analyzed) return set_err(h, UNO_KKT_ERR_STATE, "factorize before analyze");
@@ -1335,6 +1355,14 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     } else if (values_on_device) {
         h->values_ptr = values;
     } else {
+        // option pin_host_values: the caller's buffer is page-locked once (hipHostRegister) so every later
+        // upload is a direct DMA; it is unregistered when the pointer changes or the handle is destroyed
+        if (h->pin_host && S.nnz > 0 && values != h->pinned_ptr) {
+            if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
+            h->pinned_ptr = hipHostRegister(const_cast<double*>(values), S.nnz * sizeof(double), hipHostRegisterDefault) ==
+                                    hipSuccess ? values : nullptr;
+            (void)hipGetLastError();
+        }
         if (S.nnz > 0)
             HIPCHK(h, hipMemcpyAsync(h->values.p, values, S.nnz * sizeof(double), hipMemcpyHostToDevice, h->stream));
         h->values_ptr = h->values.p;

@@ -41,7 +41,7 @@ class KKTStats(ctypes.Structure):
 
 EXPORTED_SYMBOLS = [
     "uno_kkt_create", "uno_kkt_destroy", "uno_kkt_set_option", "uno_kkt_analyze", "uno_kkt_factorize",
-    "uno_kkt_set_values", "uno_kkt_fill_values", "uno_kkt_inertia", "uno_kkt_solve", "uno_kkt_stats",
+    "uno_kkt_set_values", "uno_kkt_fill_values", "uno_kkt_factorize_update", "uno_kkt_inertia", "uno_kkt_solve", "uno_kkt_stats",
     "uno_kkt_kernel_times", "uno_kkt_reset_kernel_times", "uno_kkt_stream", "uno_kkt_last_error",
     "uno_kkt_version", "uno_kkt_comm_unique_id", "uno_kkt_attach_rccl", "uno_kkt_group_create",
     "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info", "uno_kkt_rhs_setup",
@@ -78,6 +78,7 @@ def load_library():
     lib.uno_kkt_set_option.argtypes = [vp, ctypes.c_char_p, ctypes.c_double]
     lib.uno_kkt_analyze.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p]
     lib.uno_kkt_factorize.argtypes = [vp, ctypes.c_void_p, ctypes.c_int]
+    lib.uno_kkt_factorize_update.argtypes = [vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]
     lib.uno_kkt_set_values.argtypes = [vp, _i64p, _f64p, ctypes.c_int64]
     lib.uno_kkt_fill_values.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_double]
     lib.uno_kkt_inertia.argtypes = [vp, _i64p, _i64p, _i64p]
@@ -174,6 +175,13 @@ class HipKKT:
             self._check(self.lib.uno_kkt_factorize(self.h, v.ctypes.data_as(ctypes.c_void_p), 0))
         else:
             self._check(self.lib.uno_kkt_factorize(self.h, None, 0))
+
+    def factorize_update(self, values, first, count):
+        """Refactorize after a host edit of positions [first, first+count) of `values` (the array of the
+        previous host factorization): only that range is uploaded."""
+        v, _ = _f64(values)
+        self._v_keep = v
+        self._check(self.lib.uno_kkt_factorize_update(self.h, v.ctypes.data_as(ctypes.c_void_p), int(first), int(count)))
 
     def fill_values(self, first, count, value):
         self._check(self.lib.uno_kkt_fill_values(self.h, int(first), int(count), float(value)))
