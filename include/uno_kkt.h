@@ -131,6 +131,16 @@ int uno_kkt_rhs_setup(uno_kkt_t handle, int64_t n_vars, int64_t n_cons, int64_t 
 int uno_kkt_assemble_rhs(uno_kkt_t handle, const double* grad, const double* cons, const double* y,
                          const double* jac_values, double* rhs);
 
+/* Barrier diagonal Sigma on the device, PrimalDualInteriorPointProblem::evaluate_lagrangian_hessian
+ * (PrimalDualInteriorPointProblem.cpp:56-78): uno_kkt_barrier_setup takes the variable bounds once (HOST
+ * arrays, +-inf = unbounded) and lists the variables with a finite bound in ascending order (the order Uno
+ * inserts their diagonal terms); uno_kkt_assemble_barrier writes, for the t-th of them,
+ * values[t] = 0 + zl[i] / (x[i] - lb[i]) [finite lb] + zu[i] / (x[i] - ub[i]) [finite ub] (DEVICE pointers;
+ * `values` points at the first barrier entry of the COO value array).  uno_kkt_barrier_count: how many. */
+int uno_kkt_barrier_setup(uno_kkt_t handle, int64_t n_vars, const double* lb, const double* ub);
+int64_t uno_kkt_barrier_count(uno_kkt_t handle);
+int uno_kkt_assemble_barrier(uno_kkt_t handle, const double* x, const double* zl, const double* zu, double* values);
+
 /* Primal-dual direction, PrimalDualInteriorPointProblem::assemble_primal_dual_direction
  * (PrimalDualInteriorPointProblem.cpp:173-194) with compute_bound_dual_direction (:262-278) and the
  * fraction-to-boundary rules (:281-325), tau = max(tau_min, 1 - barrier_parameter): dx = sol[0:n],

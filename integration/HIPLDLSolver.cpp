@@ -24,7 +24,7 @@ namespace uno {
          const char* env = std::getenv("UNO_KKT_OPTIONS");
          if (env == nullptr || std::strstr(env, "delay_relaxed") == nullptr) uno_kkt_set_option(h, "delay_relaxed", 0.0);
          // the plugin owns its COO storage (MUMPSSolver.hpp:52): page-lock it once for direct uploads
-         uno_kkt_set_option(h, "pin_host_values", 1.0);
+         if (env == nullptr || std::strstr(env, "pin_host_values") == nullptr) uno_kkt_set_option(h, "pin_host_values", 1.0);
          return h;
       }
       void hip_destroy(void* h) { uno_kkt_destroy(static_cast<uno_kkt_t>(h)); }

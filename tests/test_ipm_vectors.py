@@ -139,3 +139,40 @@ def test_device_symv_and_quadratic_product():
     v2[:nv] = 2.0
     torch.cuda.synchronize()
     np.testing.assert_allclose(Y.cpu().numpy(), ipm_oracle.symv(n, r, c, v2, x), rtol=1e-12, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_device_barrier_diagonal_bitwise():
+    """Sigma on the device (uno_kkt_assemble_barrier) equals the host expression of
+    PrimalDualInteriorPointProblem.cpp:62-77 bit for bit: 0 + zl / (x - lb) [finite lb] + zu / (x - ub)
+    [finite ub], one entry per variable with a finite bound, ascending, written at the barrier block of the
+    COO value array (the rest of the array untouched)."""
+    import torch
+    import uno_amd
+    rng = np.random.default_rng(9)
+    n = 50000
+    x = rng.uniform(-1, 1, n)
+    lb = np.where(rng.random(n) < 0.6, x - 10.0 ** rng.uniform(-8, 1, n), -np.inf)
+    ub = np.where(rng.random(n) < 0.4, x + 10.0 ** rng.uniform(-8, 1, n), np.inf)
+    zl = rng.uniform(1e-9, 1, n)
+    zu = -rng.uniform(1e-9, 1, n)
+    bounded = np.isfinite(lb) | np.isfinite(ub)
+    ref = []
+    for i in np.nonzero(bounded)[0]:
+        d = 0.0
+        if np.isfinite(lb[i]):
+            d += zl[i] / (x[i] - lb[i])
+        if np.isfinite(ub[i]):
+            d += zu[i] / (x[i] - ub[i])
+        ref.append(d)
+    g = uno_amd.HipKKT(0)
+    assert g.barrier_setup(lb, ub) == bounded.sum()
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    X, ZL, ZU = d(x), d(zl), d(zu)
+    vals = torch.full((bounded.sum() + 10,), 7.0, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    g.assemble_barrier(X.data_ptr(), ZL.data_ptr(), ZU.data_ptr(), vals.data_ptr() + 8 * 5)
+    torch.cuda.synchronize()
+    out = vals.cpu().numpy()
+    np.testing.assert_array_equal(out[5:5 + bounded.sum()], np.array(ref))
+    assert (out[:5] == 7.0).all() and (out[5 + bounded.sum():] == 7.0).all()

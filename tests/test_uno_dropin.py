@@ -28,11 +28,16 @@ def _driver_present(request):
     pytest.skip("drop-in driver not built (needs /root/reference)")
 
 
+def drive(args, timeout):
+    """Run the drop-in driver; its last JSON line, or a failure carrying its exit status and stderr."""
+    out = subprocess.run([DRIVER] + args + ["logger=SILENT"], capture_output=True, text=True, timeout=timeout)
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert lines, f"driver {args} exited {out.returncode} without a result:\n{out.stderr[-3000:]}"
+    return json.loads(lines[-1])
+
+
 def run(solver):
-    out = subprocess.run([DRIVER, "hs015", f"linear_solver={solver}", "logger=SILENT"], capture_output=True,
-                         text=True, timeout=120)
-    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
-    return json.loads(line)
+    return drive(["hs015", f"linear_solver={solver}"], 120)
 
 
 def test_golden_matches_survey_probe():
@@ -71,10 +76,7 @@ NL_GOLDEN = {m: json.load(open(os.path.join(ROOT, "tests", "golden", f"{m}_nl_un
 
 def run_nl(model, solver):
     path = os.path.join(ROOT, "tests", "golden", f"{model}.nl")
-    out = subprocess.run([DRIVER, path, f"linear_solver={solver}", "logger=SILENT"], capture_output=True, text=True,
-                         timeout=120)
-    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
-    return json.loads(line)
+    return drive([path, f"linear_solver={solver}"], 120)
 
 
 DUALS = ("constraint_multipliers", "lower_bound_multipliers", "upper_bound_multipliers")
@@ -168,10 +170,7 @@ ABI_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "arrowband_ine
 
 
 def run_model(model, solver):
-    out = subprocess.run([DRIVER, model, f"linear_solver={solver}", "logger=SILENT"], capture_output=True, text=True,
-                         timeout=300)
-    line = [l for l in out.stdout.splitlines() if l.startswith("{")][-1]
-    return json.loads(line)
+    return drive([model, f"linear_solver={solver}"], 300)
 
 
 def same_large_run(r, g, rel=1e-10):
@@ -239,9 +238,7 @@ CVX_GOLDEN = json.load(open(os.path.join(ROOT, "tests", "golden", "convexify_uno
 
 def run_convexify(model, solver):
     path = os.path.join(ROOT, "tests", "golden", model) if model.endswith(".nl") else model
-    out = subprocess.run([DRIVER, "convexify:" + path, f"linear_solver={solver}", "logger=SILENT"], capture_output=True,
-                         text=True, timeout=600)
-    return json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][-1])
+    return drive(["convexify:" + path, f"linear_solver={solver}"], 600)
 
 
 def same_convexification(r, g):

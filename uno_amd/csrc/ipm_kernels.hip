@@ -165,6 +165,32 @@ __global__ void k_sum(const double* __restrict__ v, int64_t n, double* __restric
     }
 }
 
+// Barrier diagonal, PrimalDualInteriorPointProblem::evaluate_lagrangian_hessian
+// (PrimalDualInteriorPointProblem.cpp:56-78): for the t-th variable with a finite bound (ascending, the order
+// Uno inserts them), Sigma = 0 + zl / (x - lb) [finite lb] + zu / (x - ub) [finite ub], written into the COO
+// value array at values[first + t] -- the same operations in the same order as the host, so bit-identical.
+__global__ void k_barrier(const int32_t* __restrict__ var, const int8_t* __restrict__ which, const double* __restrict__ lb,
+                          const double* __restrict__ ub, const double* __restrict__ x, const double* __restrict__ zl,
+                          const double* __restrict__ zu, int64_t count, double* __restrict__ values) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t i = var[t];
+        const int8_t w = which[t];
+        double d = 0.;
+        if (w & 1) d += zl[i] / (x[i] - lb[i]);
+        if (w & 2) d += zu[i] / (x[i] - ub[i]);
+        values[t] = d;
+    }
+}
+
+hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double* lb, const double* ub, const double* x,
+                          const double* zl, const double* zu, int64_t count, double* values, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    int64_t g = (count + 255) / 256;
+    hipLaunchKernelGGL(k_barrier, dim3((unsigned)(g > 4096 ? 4096 : g)), dim3(256), 0, s, var, which, lb, ub, x, zl, zu,
+                       count, values);
+    return hipGetLastError();
+}
+
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
                       const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s) {
     if (n + m == 0) return hipSuccess;

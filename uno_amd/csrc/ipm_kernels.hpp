@@ -41,6 +41,8 @@ struct SymvArgs {
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
                       const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s);
 hipError_t launch_direction(const DirArgs& A, hipStream_t s);
+hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double* lb, const double* ub, const double* x,
+                          const double* zl, const double* zu, int64_t count, double* values, hipStream_t s);
 hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s);
 
 }  // namespace ukkt

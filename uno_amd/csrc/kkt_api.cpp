@@ -8,6 +8,7 @@
 
 #include <algorithm>
 #include <cfloat>
+#include <cmath>
 #include <chrono>
 #include <cstdio>
 #include <cstring>
@@ -112,6 +113,14 @@ struct uno_kkt {
     hipEvent_t ev_scale = nullptr, ev_norm = nullptr;
     int overlap_norm = 1;
     bool exact_next = false, last_optimistic = false;
+    // ||A_pre||_inf is needed only when some accepted pivot could lie at or below the null threshold.  After
+    // the last equilibration sweep every scaled entry is at most 1 (|s a_ij s| <= min(r_i, r_j) /
+    // sqrt(r_i r_j) with the sweep's row maxima r), so ||A_pre||_inf <= max row length: a factorization
+    // run with threshold 0 whose smallest accepted pivot exceeds eps * null_fac * max_row_len is the
+    // exact one and the row-sum pass is skipped (norm_valid = false).
+    bool norm_valid = false;
+    int64_t max_row_len = 0, norm_skips = 0;
+    ScanArgs scan{};  // the last factorization's scan arguments (row sums on demand)
     int64_t exact_redos = 0;
     AnalysisOptions aopt;
     double u = 0.01, null_fac = 1e-5;
@@ -178,6 +187,10 @@ struct uno_kkt {
     // device-side vector work around the solve
     int64_t rhs_n = -1, rhs_m = -1;
     DBuf<int64_t> jv_ptr;                 // per variable: range into jv_ent (Jacobian entries, constraint-ascending)
+    DBuf<int32_t> bar_var;                // barrier diagonal: bounded variables (ascending)
+    DBuf<int8_t> bar_which;               // 1: finite lower, 2: finite upper bound
+    DBuf<double> bar_lb, bar_ub;
+    int64_t bar_n = -1;
     DBuf<int32_t> jv_ent, j_con;
     DBuf<unsigned long long> alpha;
     DBuf<double> symv_tmp, symv_part, dot_d;
@@ -614,10 +627,22 @@ int sync_and_verify(uno_kkt_t h) {
         HIPCHK(h, hipStreamSynchronize(h->stream));
     }
     if (h->last_optimistic) {
-        HIPCHK(h, hipEventSynchronize(h->ev_norm));
         double anorm, mp;
-        memcpy(&anorm, h->h_counters + 9, 8);
         memcpy(&mp, h->h_counters + 8, 8);
+        const double bound = DBL_EPSILON * h->null_fac * (double)h->max_row_len * (1.0 + 1e-9);
+        if (mp > bound && h->scale_iters > 0) {  // no pivot near any possible threshold: exact as it stands
+            h->norm_skips++;
+            flush_timing(h);
+            return UNO_KKT_OK;
+        }
+        {
+            TimerScope t2(h, KC_ROWSUM);
+            HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
+        }
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 9, h->anorm.p, 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->norm_valid = true;
+        memcpy(&anorm, h->h_counters + 9, 8);
         const double thres = DBL_EPSILON * h->null_fac * anorm;
         if (!(mp > thres)) {
             h->exact_next = true;
@@ -932,8 +957,10 @@ int upload_structure(uno_kkt_t h) {
     {
         std::vector<int32_t> lr;
         h->max_long = 0;
+        h->max_row_len = 0;
         for (int64_t i = 0; i < n; ++i) {
             int64_t len = (S.cptr[i + 1] - S.cptr[i]) + (S.rptr[i + 1] - S.rptr[i]);
+            h->max_row_len = std::max(h->max_row_len, len);
             if (len > kLongRow) { lr.push_back((int32_t)i); h->max_long = std::max(h->max_long, len); }
         }
         h->n_long = (int32_t)lr.size();
@@ -1029,20 +1056,17 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.uvalR = h->uvalR.p; SA.rowpartner = h->rowpartner.p; SA.long_cnt = h->long_cnt.p;
         SA.scale_out = h->rmax.p;  // scratch of the double-buffered sweeps (new numbering); final scaling after them
         SA.scale_in = h->w.p;      // (free until the solve)
+        h->scan = SA;
+        h->norm_valid = false;
         if (h->world == 1 && h->overlap_norm && !h->exact_next) {
+            // threshold 0 and a record of the smallest accepted pivot; the row sums only if it is small
+            // (sync_and_verify)
             HIPCHK(h, launch_scale_sweeps(SA, h->scale_iters, h->rmax.p, s));
-            HIPCHK(h, hipEventRecord(h->ev_scale, s));
-            HIPCHK(h, hipStreamWaitEvent(h->stream2, h->ev_scale, 0));
-            {
-                TimerScope t2(h, KC_ROWSUM, h->stream2);
-                HIPCHK(h, launch_rowsum_norm(SA, h->rowsum.p, h->stream2));
-            }
-            HIPCHK(h, hipMemcpyAsync(h->h_counters + 9, h->anorm.p, 8, hipMemcpyDeviceToHost, h->stream2));
-            HIPCHK(h, hipEventRecord(h->ev_norm, h->stream2));
             h->last_optimistic = true;
         } else if (h->world == 1) {
             HIPCHK(h, launch_scale(SA, h->scale_iters, h->rmax.p, h->rowsum.p, s));
             h->last_optimistic = false;
+            h->norm_valid = true;
         } else {
             h->last_optimistic = false;
             int rc = dist_scale(h, SA);
@@ -1643,6 +1667,11 @@ int uno_kkt_debug_scaling(uno_kkt_t h, double* scale, double* anorm) {
     }
     if (!h->factored && h->st.factorizations == 0) return set_err(h, UNO_KKT_ERR_STATE, "no factorization");
     HIPCHK(h, hipSetDevice(h->device));
+    if (h->world == 1 && !h->norm_valid && h->scan.n > 0) {  // skipped by the bound: compute it now
+        HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
+        HIPCHK(h, hipStreamSynchronize(h->stream));
+        h->norm_valid = true;
+    }
     if (h->S.n > 0) HIPCHK(h, hipMemcpy(scale, h->scale.p, sizeof(double) * h->S.n, hipMemcpyDeviceToHost));
     unsigned long long b = 0;
     HIPCHK(h, hipMemcpy(&b, h->anorm.p, sizeof(b), hipMemcpyDeviceToHost));
@@ -1682,6 +1711,39 @@ int uno_kkt_rhs_setup(uno_kkt_t h, int64_t n_vars, int64_t n_cons, int64_t nnz_j
     HIPCHK(h, hipStreamSynchronize(s));
     h->rhs_n = n_vars;
     h->rhs_m = n_cons;
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_barrier_setup(uno_kkt_t h, int64_t n_vars, const double* lb, const double* ub) {
+    if (!h || n_vars < 0 || (n_vars > 0 && (!lb || !ub))) return UNO_KKT_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    std::vector<int32_t> var;
+    std::vector<int8_t> which;
+    for (int64_t i = 0; i < n_vars; ++i) {  // is_finite (uno/tools/Infinity.hpp): |b| < INF
+        const int8_t w = (int8_t)((std::fabs(lb[i]) < INFINITY ? 1 : 0) | (std::fabs(ub[i]) < INFINITY ? 2 : 0));
+        if (w) { var.push_back((int32_t)i); which.push_back(w); }
+    }
+    hipStream_t s = h->stream;
+    HIPCHK(h, h->bar_var.upload(var, s));
+    HIPCHK(h, h->bar_which.upload(which, s));
+    HIPCHK(h, h->bar_lb.alloc(std::max<int64_t>(n_vars, 1)));
+    HIPCHK(h, h->bar_ub.alloc(std::max<int64_t>(n_vars, 1)));
+    if (n_vars > 0) {
+        HIPCHK(h, hipMemcpyAsync(h->bar_lb.p, lb, sizeof(double) * n_vars, hipMemcpyHostToDevice, s));
+        HIPCHK(h, hipMemcpyAsync(h->bar_ub.p, ub, sizeof(double) * n_vars, hipMemcpyHostToDevice, s));
+    }
+    HIPCHK(h, hipStreamSynchronize(s));
+    h->bar_n = (int64_t)var.size();
+    return UNO_KKT_OK;
+}
+
+int64_t uno_kkt_barrier_count(uno_kkt_t h) { return h ? h->bar_n : -1; }
+
+int uno_kkt_assemble_barrier(uno_kkt_t h, const double* x, const double* zl, const double* zu, double* values) {
+    if (!h || !x || !zl || !zu || !values) return UNO_KKT_ERR_ARG;
+    if (h->bar_n < 0) return set_err(h, UNO_KKT_ERR_STATE, "assemble_barrier before barrier_setup");
+    HIPCHK(h, hipSetDevice(h->device));
+    HIPCHK(h, launch_barrier(h->bar_var.p, h->bar_which.p, h->bar_lb.p, h->bar_ub.p, x, zl, zu, h->bar_n, values, h->stream));
     return UNO_KKT_OK;
 }
 

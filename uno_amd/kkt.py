@@ -46,6 +46,7 @@ EXPORTED_SYMBOLS = [
     "uno_kkt_version", "uno_kkt_comm_unique_id", "uno_kkt_attach_rccl", "uno_kkt_group_create",
     "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info", "uno_kkt_rhs_setup",
     "uno_kkt_assemble_rhs", "uno_kkt_assemble_direction", "uno_kkt_symv", "uno_kkt_quadratic_product",
+    "uno_kkt_barrier_setup", "uno_kkt_barrier_count", "uno_kkt_assemble_barrier",
 ]
 
 
@@ -99,6 +100,10 @@ def load_library():
     lib.uno_kkt_attach_local.argtypes = [vp, vp, ctypes.c_int]
     lib.uno_kkt_dist_info.argtypes = [vp, ctypes.POINTER(KKTDistInfo)]
     lib.uno_kkt_debug_scaling.argtypes = [vp, _f64p, _f64p]
+    lib.uno_kkt_barrier_setup.argtypes = [vp, ctypes.c_int64, _f64p, _f64p]
+    lib.uno_kkt_barrier_count.argtypes = [vp]
+    lib.uno_kkt_barrier_count.restype = ctypes.c_int64
+    lib.uno_kkt_assemble_barrier.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.uno_kkt_debug_partition.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _i64p]
     lib.uno_kkt_debug_partition.restype = ctypes.c_int64
@@ -212,6 +217,19 @@ class HipKKT:
         an = ctypes.c_double()
         self._check(self.lib.uno_kkt_debug_scaling(self.h, sc.ctypes.data_as(_f64p), ctypes.byref(an)))
         return sc, an.value
+
+    def barrier_setup(self, lb, ub):
+        """Bounds of the variables (host), PrimalDualInteriorPointProblem.cpp:56-78; returns the number of
+        barrier diagonal entries."""
+        lb, lbp = _f64(lb)
+        ub, ubp = _f64(ub)
+        self._check(self.lib.uno_kkt_barrier_setup(self.h, len(lb), lbp, ubp))
+        return int(self.lib.uno_kkt_barrier_count(self.h))
+
+    def assemble_barrier(self, x_ptr, zl_ptr, zu_ptr, values_ptr):
+        """Sigma into the COO values at values_ptr (all DEVICE addresses)."""
+        self._check(self.lib.uno_kkt_assemble_barrier(self.h, ctypes.c_void_p(int(x_ptr)), ctypes.c_void_p(int(zl_ptr)),
+                                                      ctypes.c_void_p(int(zu_ptr)), ctypes.c_void_p(int(values_ptr))))
 
     def stats(self):
         s = KKTStats()
