@@ -166,6 +166,34 @@ def test_random_indefinite(uno_amd, nmax, dens):
     assert done >= 6
 
 
+@pytest.mark.parametrize("mf", [0, 1])
+def test_tile_kernels(uno_amd, mf):
+    """One-wave fronts on either front kernel (option mfma_fronts: the matrix-core tile kernels
+    k_factor_mf / k_factor_df_mf, or the register-grid kernels): inertia equal to the oracle's and the
+    residual bar, on dense indefinite fronts up to 64 rows with zero diagonals (2x2 pivots, interchanges,
+    LDS steps in the middle of a panel) and on the C2 arrowband KKT (level launches + dataflow launch)."""
+    from uno_amd import arrowband, SEEDS
+    rng = np.random.default_rng(17 + mf)
+    done = 0
+    for trial in range(16):
+        n = int(rng.integers(5, 65))
+        rr, cc, vv, S = random_sym(rng, n, 0.5, zero_diag_frac=0.6)
+        ev = np.linalg.eigvalsh(S)
+        if np.min(abs(ev)) < 1e-8 * max(1.0, abs(ev).max()):
+            continue
+        g, o = both(n, rr, cc, vv, mfma_fronts=mf)
+        assert g.inertia() == o.inertia() == (int((ev > 0).sum()), int((ev < 0).sum()), 0)
+        b = rng.standard_normal(n)
+        np.testing.assert_allclose(S @ g.solve(b), b, atol=1e-8 * np.linalg.cond(S) * np.abs(b).max())
+        done += 1
+    assert done >= 8
+    n, nv, m, r, c, v, b = arrowband(10000, SEEDS["C2"])
+    g, o = both(n, r, c, v, mfma_fronts=mf)
+    assert g.inertia() == o.inertia()
+    xg = g.solve(b)
+    assert rel_residual(n, r, c, v, xg, b) < RES_TOL
+
+
 def test_arrowband_c2(uno_amd):
     """C2: arrowband KKT N=1e4; first factorization has wrong inertia (negative
     curvature), so the values of one regularized retry are compared too."""

@@ -14,7 +14,7 @@ import sqlite3
 import sys
 
 GROUPS = {
-    "factor": ("k_factor_lds", "k_factor_global", "k_factor_df"),
+    "factor": ("k_factor_lds", "k_factor_global", "k_factor_df", "k_factor_mf", "k_big_"),
     "solve": ("k_solve_fwd", "k_solve_bwd"),
     "pack": ("k_pack",),
     "scale": ("k_rowscan", "k_normmax", "k_scale_update"),
@@ -62,8 +62,23 @@ def pmc(db, out):
     print(json.dumps(res, indent=1))
 
 
+def bykernel(db):
+    """per kernel name: every counter summed over its dispatches, divided by the dispatch count"""
+    c = sqlite3.connect(db)
+    rows = c.execute("select kernel_name, counter_name, sum(value), count(distinct dispatch_id) "
+                     "from counters_collection group by kernel_name, counter_name order by kernel_name").fetchall()
+    cur = None
+    for name, cn, s, cnt in rows:
+        if name != cur:
+            cur = name
+            print(f"{name[:70]}  ({cnt} dispatches)")
+        print(f"    {cn:28s} {s / max(cnt, 1):16.0f} per dispatch")
+
+
 if __name__ == "__main__":
-    if sys.argv[1] == "stats":
+    if sys.argv[1] == "bykernel":
+        bykernel(sys.argv[2])
+    elif sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     else:
         pmc(sys.argv[2], sys.argv[3])

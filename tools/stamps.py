@@ -42,6 +42,14 @@ if os.environ.get("MODE") == "4":
         print(f"level {lev:2d} m {fm[s].mean():5.1f} | assembly: rows+zero {a0.mean():6.2f} entries {a1.mean():6.2f} "
               f"children {a2.mean():6.2f} us (total {asm[s].mean():6.2f})")
     sys.exit(0)
+if os.environ.get("MODE") == "5":  # tile kernels: shader cycles per front of each phase
+    for lev in range(fl.max() + 1):
+        s = fl == lev
+        c = st[s, 4:8].astype(np.float64)
+        print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | cycles/front: extract {c[:,0].mean():7.0f} "
+              f"pivots {c[:,1].mean():7.0f} stage+mfma {c[:,2].mean():7.0f} lds-steps {c[:,3].mean():7.0f} | "
+              f"assemble {asm[s].mean():6.2f} loop {loop[s].mean():6.2f} write {wout[s].mean():5.2f} us")
+    sys.exit(0)
 if os.environ.get("MODE") == "3":
     w4, w5 = st[:, 4], st[:, 5]
     parts = np.stack([w4 & 0xffffffff, w4 >> 32, w5 & 0xffffffff, w5 >> 32, st[:, 6]], 1).astype(np.float64)

@@ -197,6 +197,7 @@ struct uno_kkt {
     DBuf<double> xtmp, rtmp;              // host-pointer solves / refinement residuals
     int refine = 1;                       // refinement steps after a factorization with relaxed pivots
     int pin_host = 0;                     // option pin_host_values
+    int mfma_fronts = 0;                  // option mfma_fronts: one-wave fronts on the matrix-core tile kernels
     const double* pinned_ptr = nullptr;   // caller buffer registered with hipHostRegister
     DBuf<int64_t> edit_pos;               // uno_kkt_set_values staging
     DBuf<double> edit_val;
@@ -1082,6 +1083,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
+    A.mf = h->mfma_fronts;
     A.big = h->big.p;
     if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
@@ -1241,6 +1243,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
     else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "pin_host_values") h->pin_host = value != 0.0;
+    else if (n == "mfma_fronts") h->mfma_fronts = value != 0.0;
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else if (n == "gather_solution") h->gather_solution = value != 0.0;

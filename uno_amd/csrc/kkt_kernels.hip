@@ -24,6 +24,8 @@ namespace ukkt {
 constexpr int kThreads = 256;
 template <int NT> constexpr int kGrid = NT == 64 ? 8 : 16;  // side of the Schur-update thread grid
 
+typedef double dbl4 __attribute__((ext_vector_type(4)));  // v_mfma_f64_16x16x4f64 accumulator
+
 enum : int8_t { PIV_NULL = 0, PIV_1X1 = 1, PIV_2X2_A = 2, PIV_2X2_B = 3, PIV_STUCK = 4 };
 
 __device__ __forceinline__ double as_double(unsigned long long b) { return __longlong_as_double((long long)b); }
@@ -1316,6 +1318,442 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
 }
 
 // ------------------------------------------------------------------------------------------------
+// One-wave front factorization on matrix-core tiles (fronts of m <= 16 * TR rows)
+// ------------------------------------------------------------------------------------------------
+// The front lives in registers as the lower triangle of TR x TR tiles of 16 x 16 in the
+// v_mfma_f64_16x16x4f64 C layout (lane l: column l & 15, rows (l >> 4) + 4 r; MI355X_MICROARCH.md,
+// f64 MFMA).  Fully-summed columns are eliminated in panels of at most one tile column: the panel is
+// transposed through an LDS stage into a row-per-lane copy P (lane i = row i), where a pivot step is
+// one per-lane threshold compare + one ballot (the Duff-Reid 1x1 rule of factor_front's fast path),
+// one division and the update of the panel's later pivot columns with readlane operands -- no LDS
+// round trip per pivot.  L of each pivot goes to HBM at once.  At the end of the panel the eliminated
+// columns W (staged in LDS) update every trailing tile on the matrix cores, C -= W (W D^-1)^T: the
+// same products A(i,k) * (A(j,k) / d_k) as the one-pivot updates.  A pivot that fails the quick test
+// flushes the pending update, spills the live tiles to the packed LDS front and takes one LDS step of
+// the full search (interchanges, 2x2, null pivots, relaxation, delays) before the tiles are reloaded.
+constexpr int kStageLd = 17;  // row stride (doubles) of the LDS panel stage
+
+// doubles of the front region of the tile kernels: the packed triangle or the panel stage (rows of
+// whole tiles), whichever is larger; monotone in m, so factor_lds_bytes(mmax) covers every m <= mmax
+__host__ __device__ __forceinline__ int64_t mf_front_doubles(int m) {
+    const int64_t pk = (((int64_t)m * (m + 1) / 2) + 1) & ~1ll;
+    const int64_t sg = (((int64_t)16 * ((m + 15) >> 4) * kStageLd) + 1) & ~1ll;
+    return pk > sg ? pk : sg;
+}
+
+template <int TR>
+__device__ __forceinline__ void mf_load(const PackedStore& st, int m, dbl4 (&acc)[TR * (TR + 1) / 2]) {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int g = lane >> 4, c = lane & 15;
+    const int ntr = (m + 15) >> 4;
+#pragma unroll
+    for (int tr = 0; tr < TR; ++tr) {
+        if (tr >= ntr) break;  // uniform
+#pragma unroll
+        for (int tc = 0; tc < TR; ++tc) {
+            if (tc > tr) break;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * tr + g + 4 * r, j = 16 * tc + c;
+                const bool ok = i < m && j <= i;
+                const double v = st.F[ok ? st.idx(i, j) : -1];
+                acc[tr * (tr + 1) / 2 + tc][r] = ok ? v : 0.0;
+            }
+        }
+    }
+}
+
+// live part (columns >= k) of the tiles -> packed LDS front
+template <int TR>
+__device__ __forceinline__ void mf_spill(const PackedStore& st, int m, int k, const dbl4 (&acc)[TR * (TR + 1) / 2]) {
+    int lane = threadIdx.x & 63;
+    asm volatile("" : "+v"(lane));
+    const int g = lane >> 4, c = lane & 15;
+    const int ntr = (m + 15) >> 4;
+#pragma unroll
+    for (int tr = 0; tr < TR; ++tr) {
+        if (tr >= ntr) break;
+#pragma unroll
+        for (int tc = 0; tc < TR; ++tc) {
+            if (tc > tr) break;
+            if (16 * tc + 15 < k) continue;  // uniform: tile column entirely eliminated
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int i = 16 * tr + g + 4 * r, j = 16 * tc + c;
+                st.F[(i < m && j >= k && j <= i) ? st.idx(i, j) : -1] = acc[tr * (tr + 1) / 2 + tc][r];
+            }
+        }
+    }
+}
+
+// A later LDS step interchanged rows a < b: the L columns [0, ncols) already in HBM trade those rows.
+// This wave's stores are drained first and the rows are read back through L2 (sc1).
+__device__ __forceinline__ void mf_swap_L(double* Lf, int m, int ncols, int a, int b) {
+    drain_stores();
+    for (int j = threadIdx.x & 63; j < ncols; j += 64) {
+        double* Lj = Lf + (int64_t)j * m - (int64_t)j * (j - 1) / 2 - j;
+        const double x = ld_sc1(Lj + a), y = ld_sc1(Lj + b);
+        Lj[a] = y;
+        Lj[b] = x;
+    }
+    drain_stores();
+}
+
+// L of the column(s) [k, k + nk) eliminated by an LDS step, from the packed front (factor_front's
+// write-out formulas: D on the diagonal / 2x2 block, L(i, j) = cA A(i, base) + cB A(i, base + 1))
+__device__ __forceinline__ void mf_write_L_lds(const PackedStore& st, double* Lf, int m, int k, int nk, const int8_t* piv) {
+    const int lane = threadIdx.x & 63;
+    for (int j = k; j < k + nk; ++j) {
+        const int8_t kind = piv[j];
+        double ca = 0.0, cbv = 0.0;
+        int base = j;
+        if (kind == PIV_1X1) {
+            ca = 1.0 / st.at(j, j);
+        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+            const int k0 = kind == PIV_2X2_A ? j : j - 1;
+            const double a = st.at(k0, k0), b = st.at(k0 + 1, k0), e = st.at(k0 + 1, k0 + 1);
+            const double idet = 1.0 / (a * e - b * b);
+            if (kind == PIV_2X2_A) { ca = e * idet; cbv = -b * idet; }
+            else { ca = -b * idet; cbv = a * idet; base = j - 1; }
+        }
+        double* Lj = Lf + (int64_t)j * m - (int64_t)j * (j - 1) / 2 - j;
+        for (int i = j + lane; i < m; i += 64) {
+            double v;
+            if (i == j) v = kind == PIV_NULL ? 0.0 : st.at(j, j);
+            else if (kind == PIV_2X2_A && i == j + 1) v = st.at(j + 1, j);
+            else {
+                v = ca * st.at(i, base);
+                if (kind >= PIV_2X2_A) v += cbv * st.at(i, base + 1);
+            }
+            Lj[i] = v;
+        }
+    }
+}
+
+template <int TR, bool DF>
+__device__ void factor_front_mf(const PackedStore& st, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
+                                double* dinvs, const FactorArgs& A, int f, FrontShared* sh) {
+    constexpr int NTL = TR * (TR + 1) / 2;
+    constexpr int RPL = (16 * TR + 63) / 64;  // panel rows per lane
+    const int tid = threadIdx.x;
+    const int lane = tid & 63, g = lane >> 4, cl = lane & 15;
+    const int ntr = (m + 15) >> 4;
+    for (int i = tid; i < m; i += 64) lorig[i] = i;
+    __syncthreads();
+    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+    double minpiv = INFINITY;
+    long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
+    bool delays_recorded = false;
+    double* Lf = A.L + A.L_off[f];
+    double* S = st.F;  // panel stage: aliases the packed front, dead while the tiles hold the front
+    dbl4 acc[NTL];
+    mf_load<TR>(st, m, acc);
+    // diagnostics (stamp_mode 5): shader cycles of extraction / pivots / stage + MFMA / LDS steps
+    const bool stamping = A.stamps != nullptr && A.stamp_mode == 5;
+    unsigned long long cyc[4] = {0, 0, 0, 0}, t_mark = 0;
+    int k = 0;
+    while (k < p) {
+        if (stamping) t_mark = __builtin_amdgcn_s_memtime();
+        const int tc = k >> 4, j0 = k & 15;
+        const int jlim = min(16, p - 16 * tc);  // panel: pivot columns [16 tc + j0, 16 tc + jlim)
+        // ---- tile column tc -> LDS stage -> row-per-lane panel P (upper part and rows >= m zero) ----
+#pragma unroll
+        for (int TC = 0; TC < TR; ++TC) {
+            if (TC != tc) continue;  // uniform: static tile indices
+            int gg = g, cc = cl;
+            asm volatile("" : "+v"(gg), "+v"(cc));
+            double* dst = S + gg * kStageLd + cc;
+#pragma unroll
+            for (int tr = 0; tr < TR; ++tr) {
+                if (tr < TC) continue;
+                if (tr >= ntr) break;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) dst[(16 * tr + 4 * r) * kStageLd] = acc[tr * (tr + 1) / 2 + TC][r];
+            }
+        }
+        double P[RPL][16];
+#pragma unroll
+        for (int rr = 0; rr < RPL; ++rr) {
+            int i = lane + 64 * rr;
+            asm volatile("" : "+v"(i));  // per-section addresses (not hoisted into live registers)
+            const bool rowok = i < m && i >= 16 * tc;
+            const double* src = S + (rowok ? i : 16 * tc) * kStageLd;  // one base, immediate offsets
+            double v[16];
+#pragma unroll
+            for (int c = 0; c < 16; ++c) v[c] = src[c];
+            // keep the reads unconditional (all issued before the first wait): sunk under the masks below
+            // they become one divergent branch + LDS wait per element
+#pragma unroll
+            for (int c = 0; c < 16; ++c) asm volatile("" : "+v"(v[c]));
+            // lower part of the live columns only: upper entries, rows >= m and columns eliminated before
+            // this panel read as 0 (the update below keeps them 0: its row factor is 0 there)
+#pragma unroll
+            for (int c = 0; c < 16; ++c) P[rr][c] = (rowok && i >= 16 * tc + c && c >= j0) ? v[c] : 0.0;
+        }
+        if (stamping) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cyc[0] += t - t_mark; t_mark = t; }
+        // ---- pivots of the panel: quick 1x1 test, L to HBM, update of the later panel columns ----
+        // Column jj is broadcast through an LDS vector (the stage is free between the extraction and the
+        // W stage): the pivot and the panel's row kk come back as uniform broadcast reads, so a step costs
+        // the test, one division, the L store and one FMA per later panel column on the vector ALU.
+        double* vec = S;
+        bool need = false;
+        int jend = j0;
+#pragma unroll
+        for (int jj = 0; jj < 16; ++jj) {
+            if (jj < j0 || jj >= jlim || need) continue;  // uniform
+            const int kk = 16 * tc + jj;
+#pragma unroll
+            for (int rr = 0; rr < RPL; ++rr) vec[lane + 64 * rr] = P[rr][jj];
+            const double akk = vec[kk];
+            double sv[16];
+#pragma unroll
+            for (int c = 0; c < 16; c += 2) {  // 16-byte broadcast reads of the panel rows 16 tc .. 16 tc + 15
+                sv[c] = vec[16 * tc + c];
+                sv[c + 1] = vec[16 * tc + c + 1];
+            }
+            const double aak = fabs(akk);
+            bool bad = false;
+#pragma unroll
+            for (int rr = 0; rr < RPL; ++rr) {
+                const int i = lane + 64 * rr;
+                bad |= i > kk && i < m && A.u * fabs(P[rr][jj]) > aak;
+            }
+            need = (__ballot(bad) != 0) || !(aak > thres);
+            if (need) continue;
+            minpiv = fmin(minpiv, aak);
+            const double dinv = 1.0 / akk;
+            double* Lj = Lf + (int64_t)kk * m - (int64_t)kk * (kk - 1) / 2 - kk;  // L(i, kk) = Lj[i]
+            double li[RPL];
+#pragma unroll
+            for (int rr = 0; rr < RPL; ++rr) {
+                const int i = lane + 64 * rr;
+                const double l = P[rr][jj] * dinv;
+                li[rr] = i > kk ? l : 0.0;
+                if (i >= kk && i < m) Lj[i] = i == kk ? akk : l;
+            }
+            dinvs[kk] = dinv;  // every lane stores the same value (no divergent branch)
+            piv[kk] = PIV_1X1;
+            if (akk > 0.0) npos++; else nneg++;
+#pragma unroll
+            for (int c = 1; c < 16; ++c) {
+                if (c <= jj) continue;
+                if (c >= jlim) break;  // uniform
+#pragma unroll
+                for (int rr = 0; rr < RPL; ++rr) P[rr][c] -= li[rr] * sv[c];  // A(i,c) -= L(i,kk) A(c,kk)
+            }
+            jend = jj + 1;
+        }
+        if (stamping) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cyc[1] += t - t_mark; t_mark = t; }
+        if (jend > j0) {
+            // ---- panel columns W -> stage; trailing tiles on MFMA: C -= (W D^-1) W^T over the eliminated
+            // columns (the L side is zero for the panel columns not eliminated here) ----
+#pragma unroll
+            for (int rr = 0; rr < RPL; ++rr) {
+                int i = lane + 64 * rr;
+                asm volatile("" : "+v"(i));
+                if (i < 16 * ntr) {
+                    double* dst = S + i * kStageLd;
+#pragma unroll
+                    for (int c = 0; c < 16; ++c) dst[c] = P[rr][c];
+                }
+            }
+#pragma unroll
+            for (int TC = 0; TC < TR; ++TC) {
+                if (TC != tc) continue;
+#pragma unroll
+                for (int kc = 0; kc < 4; ++kc) {
+                    if (4 * kc + 4 <= j0 || 4 * kc >= jend) continue;  // uniform: no pivot of this k-chunk
+                    double w[TR];
+                    int gg = g, cc = cl;
+                    asm volatile("" : "+v"(gg), "+v"(cc));
+                    const double* src = S + cc * kStageLd + gg;
+#pragma unroll
+                    for (int tr = 0; tr < TR; ++tr) {
+                        if (tr < TC) continue;
+                        w[tr] = tr < ntr ? src[16 * tr * kStageLd + 4 * kc] : 0.0;  // uniform condition
+                    }
+                    const int col = 4 * kc + gg;
+                    const bool cok = col >= j0 && col < jend;
+                    const double dv = dinvs[cok ? 16 * tc + col : 0];
+                    const double dsel = cok ? -dv : 0.0;
+#pragma unroll
+                    for (int tr = 0; tr < TR; ++tr) {
+                        if (tr < TC) continue;
+                        if (tr >= ntr) break;
+                        const double lop = w[tr] * dsel;  // -L(16 tr + (l & 15), column) on the A side
+#pragma unroll
+                        for (int tcp = 0; tcp < TR; ++tcp) {
+                            if (tcp < TC) continue;
+                            if (tcp > tr) break;
+                            acc[tr * (tr + 1) / 2 + tcp] =
+                                __builtin_amdgcn_mfma_f64_16x16x4f64(lop, w[tcp], acc[tr * (tr + 1) / 2 + tcp], 0, 0, 0);
+                        }
+                    }
+                }
+            }
+        }
+        k = 16 * tc + jend;
+        if (stamping) {
+            __builtin_amdgcn_s_waitcnt(0);
+            const unsigned long long t = __builtin_amdgcn_s_memtime();
+            cyc[2] += t - t_mark;
+            t_mark = t;
+        }
+        if (!need) continue;
+        // ---- pivot k failed the quick test: one LDS step of the full search (factor_front's LDS path) ----
+        mf_spill<TR>(st, m, k, acc);
+        __syncthreads();
+        PivotDecision d = search_pivot(st, m, k, p, A.u, thres, minpiv);  // wave-uniform
+        const bool stuck = d.kind == PIV_STUCK;
+        if (stuck) { d.kind = PIV_NULL; d.c = k; }
+        if (d.c != k) {
+            sym_swap<64>(st, m, k, d.c, lrow, lorig);
+            __syncthreads();
+            mf_swap_L(Lf, m, k, k, d.c);
+        }
+        if (d.kind == PIV_2X2_A) {
+            const int r = d.r == k ? d.c : d.r;
+            if (r != k + 1) {
+                sym_swap<64>(st, m, k + 1, r, lrow, lorig);
+                __syncthreads();
+                mf_swap_L(Lf, m, k, k + 1, r);
+            }
+        }
+        if (tid == 0) {
+            if (stuck) nstuck++;
+            nrel += d.relaxed;
+            // first pivot that needed a relaxed threshold: the columns still fully summed would be delayed
+            // by MUMPS; report them (except at roots) so the host moves them to the parent
+            if (d.relaxed && !delays_recorded && A.record_delays && A.fparent[f] >= 0) {
+                delays_recorded = true;
+                unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
+                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
+            }
+        }
+        int nk;
+        if (d.kind == PIV_NULL) {
+            for (int i = k + 1 + tid; i < m; i += 64) st.at(i, k) = 0.0;
+            piv[k] = PIV_NULL;
+            nzero++;
+            nk = 1;
+        } else if (d.kind == PIV_1X1) {
+            const double dk = st.at(k, k);
+            schur_update_generic<8, false>(st, m, k, 1.0 / dk, 0.0, 0.0);
+            piv[k] = PIV_1X1;
+            if (dk > 0.0) npos++; else nneg++;
+            nk = 1;
+        } else {  // 2x2
+            const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
+            const double det = a * e - b * b;
+            const double idet = 1.0 / det;
+            schur_update_generic<8, true>(st, m, k, a * idet, b * idet, e * idet);
+            piv[k] = PIV_2X2_A;
+            piv[k + 1] = PIV_2X2_B;
+            n2++;
+            if (det < 0.0) { npos++; nneg++; }
+            else if (a + e > 0.0) npos += 2;
+            else nneg += 2;
+            nk = 2;
+        }
+        __syncthreads();
+        mf_write_L_lds(st, Lf, m, k, nk, piv);
+        k += nk;
+        mf_load<TR>(st, m, acc);
+        if (stamping) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cyc[3] += t - t_mark; }
+    }
+    if (stamping && tid == 0)
+        for (int q = 0; q < 4; ++q) A.stamps[8 * f + 4 + q] = cyc[q];
+    if (A.stamps && tid == 0) A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
+    // ---- permuted row ids and pivot kinds ----
+    for (int i = tid; i < m; i += 64) {
+        A.frow[A.rows_off[f] + i] = lrow[i];
+        A.fpos[A.rows_off[f] + lorig[i]] = i;
+        if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
+    }
+    // ---- contribution block (row-major packed lower triangle of order m - p) from the tiles ----
+    if (m > p) {
+        double* cb = A.cb + A.cb_off[f];
+#pragma unroll
+        for (int tr = 0; tr < TR; ++tr) {
+            if (tr >= ntr) break;
+            if (16 * tr + 15 < p) continue;  // uniform: tile rows entirely pivot rows
+#pragma unroll
+            for (int tc = 0; tc < TR; ++tc) {
+                if (tc > tr) break;
+                if (16 * tc + 15 < p) continue;
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int i = 16 * tr + g + 4 * r, j = 16 * tc + cl;
+                    if (i < m && j >= p && j <= i) {
+                        double* dst = cb + ((i - p) * (i - p + 1)) / 2 + (j - p);
+                        if (DF) st_sc1(dst, acc[tr * (tr + 1) / 2 + tc][r]);
+                        else *dst = acc[tr * (tr + 1) / 2 + tc][r];
+                    }
+                }
+            }
+        }
+    }
+    if (tid == 0) {
+        A.fstat[f] = (int32_t)((nstuck > 0xffff ? 0xffff : nstuck) | ((nrel > 0x7fff ? 0x7fff : nrel) << 16));
+        A.fcnt[f] = (unsigned long long)npos | (unsigned long long)nneg << 16 | (unsigned long long)nzero << 32 |
+                    (unsigned long long)n2 << 48;
+        A.fmin[f] = minpiv;
+    }
+}
+
+// LDS layout of the tile kernels: [FrontShared 32 B][front region mf_front_doubles(m)][sloc m][dinvs m]
+// [lrow m][lorig m][piv m]
+template <int TR>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TR > 2 ? 2 : 3))) void k_factor_mf(FactorArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const PackedStore st{smem + 4};
+    const int64_t fsize = mf_front_doubles(m);
+    double* sloc = smem + 4 + fsize;
+    double* dinvs = sloc + m;
+    int32_t* lrow = (int32_t*)(dinvs + m);
+    int32_t* lorig = lrow + m;
+    int8_t* pk = (int8_t*)(lorig + m);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
+    assemble_front<64, false>(st, packed_even(m), m, p, lrow, sloc, lorig, A, f);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
+    factor_front_mf<TR, false>(st, m, p, lrow, lorig, pk, dinvs, A, f, sh);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
+}
+
+// k_factor_df on the tile factorization (same ticket / arrival-counter protocol)
+template <int TR>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_df_mf(FactorArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double smem[];
+    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
+    uint32_t tk = 0;
+    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(A.df_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
+    const int t = (int)(tk - (A.df_epoch - 1u) * (uint32_t)A.df_nf);
+    if (t < 0 || t >= A.df_nf) return;
+    const int f = A.df_order[t];
+    const int m = A.fm[f], p = A.fp[f];
+    const PackedStore st{smem + 4};
+    const int64_t fsize = mf_front_doubles(m);
+    double* sloc = smem + 4 + fsize;
+    double* dinvs = sloc + m;
+    int32_t* lrow = (int32_t*)(dinvs + m);
+    int32_t* lorig = lrow + m;
+    int8_t* pk = (int8_t*)(lorig + m);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
+    assemble_front<64, true>(st, packed_even(m), m, p, lrow, sloc, lorig, A, f);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
+    factor_front_mf<TR, true>(st, m, p, lrow, lorig, pk, dinvs, A, f, sh);
+    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
+    const int par = A.fparent[f];
+    drain_stores();
+    if (par >= 0 && threadIdx.x == 0) __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------------------------------------
 // triangular solves (multifrontal, level by level)
 // ------------------------------------------------------------------------------------------------
 
@@ -2134,7 +2572,6 @@ __global__ __launch_bounds__(64) void k_xpos(SolveArgs A, DfArgs D, int32_t* __r
 // The host repeats panel + update until every front of the launch is done (one check per batch).
 constexpr int kBigNB = 32;
 
-typedef double dbl4 __attribute__((ext_vector_type(4)));
 
 // L(i, q) = ca * W(i, base) + cb * W(i, base + 1): the write-out coefficients of factor_front
 template <class S>
@@ -2595,6 +3032,11 @@ size_t factor_lds_bytes(int mmax) {
            (size_t)((mmax + 15) & ~15) + (size_t)grid_rows * sizeof(double);
 }
 
+size_t factor_lds_bytes_mf(int mmax) {
+    return 32 + (size_t)mf_front_doubles(mmax) * sizeof(double) + 2 * (size_t)mmax * sizeof(double) +
+           2 * (size_t)mmax * sizeof(int32_t) + (size_t)((mmax + 15) & ~15);
+}
+
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (global) {
@@ -2603,7 +3045,13 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
         size_t sh = factor_lds_bytes(mmax);
         // small fronts: one wave per front (no cross-wave barriers, more fronts per CU);
         // larger fronts: four waves on a 16x16 update grid
-        if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
+        if (A.mf && mmax <= 64) {  // tile kernels (matrix-core trailing updates)
+            sh = factor_lds_bytes_mf(mmax);
+            static const size_t pad = getenv("UNO_KKT_LDS_PAD") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD")) : 0;  // diagnostics
+            sh += pad;
+            if (mmax <= 32) hipLaunchKernelGGL((k_factor_mf<2>), dim3(count), dim3(64), sh, s, A, fronts);
+            else hipLaunchKernelGGL((k_factor_mf<4>), dim3(count), dim3(64), sh, s, A, fronts);
+        } else if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= 64) hipLaunchKernelGGL((k_factor_lds<64, 8>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= kMaxWaveFront) hipLaunchKernelGGL((k_factor_lds<64, 9>), dim3(count), dim3(64), sh, s, A, fronts);
         else hipLaunchKernelGGL((k_factor_lds<kThreads, 8>), dim3(count), dim3(kThreads), sh, s, A, fronts);
@@ -2719,7 +3167,9 @@ int big_panel_width() { return kBigNB; }
 
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     if (A.df_nf <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax), s, A);
+    static const size_t pad = getenv("UNO_KKT_LDS_PAD") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD")) : 0;  // diagnostics
+    if (A.mf && mmax <= 64) hipLaunchKernelGGL(k_factor_df_mf<4>, dim3(A.df_nf), dim3(64), factor_lds_bytes_mf(mmax) + pad, s, A);
+    else hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax), s, A);
     return hipGetLastError();
 }
 

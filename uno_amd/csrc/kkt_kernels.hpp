@@ -54,6 +54,7 @@ struct FactorArgs {
     int stamp_mode;  // 1: phases + cycle counts, 2: write-out sub-phases in slots 4..7  // diagnostics (nullptr in normal runs): per front 8 words
     double u;
     double null_fac;
+    int mf;                     // 1: one-wave fronts on the matrix-core tile kernels (k_factor_mf / k_factor_df_mf)
     // dataflow schedule of the upper tree (k_factor_df), after the level launches of the lower levels
     const int32_t* df_order;    // fronts, children before parents
     int32_t df_nf;
@@ -173,6 +174,7 @@ hipError_t launch_scatter64(const double* src, const int64_t* idx, double* dst, 
 hipError_t launch_neg(const double* b, double* r, int64_t n, hipStream_t s);  // r = -b
 hipError_t launch_sub(double* x, const double* d, int64_t n, hipStream_t s);   // x -= d
 size_t factor_lds_bytes(int mmax);
+size_t factor_lds_bytes_mf(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 // one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of
 // p*m - p*(p-1)/2 (rounded up to even) + m (rounded up to even) + m / 2 (int32 row positions)
