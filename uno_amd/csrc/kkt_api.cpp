@@ -138,6 +138,9 @@ struct uno_kkt {
     const double* values_ptr = nullptr;  // device values used by the last factorization
     // device arrays
     DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, rmax, bvec;
+    DBuf<int32_t> slot_src;               // k_pack: per slot its single COO position, or -1 (multi_slots)
+    DBuf<int32_t> multi_slots;            // slots with several COO positions (k_pack_multi)
+    int64_t n_multi = 0;
     DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, fstat;
     DBuf<uint32_t> ent_lpos;
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
@@ -150,7 +153,12 @@ struct uno_kkt {
     DBuf<double> fmin;
     int want_stamps = 0;
     DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed, rowpartner;
-    DBuf<double> uvalR;  // row-major copy of |A| (single-GPU equilibration)
+    DBuf<double> uvalR;  // row-major copy of |A| (single-GPU equilibration, option front_sweeps=0)
+    int front_sweeps = 1;                 // option front_sweeps: equilibration over the fronts' slots (k_sweep_front)
+    bool use_front_sweeps = false;        // front_sweeps, one GPU and every front within kMaxSweepFront rows
+    DBuf<int8_t> longpos;                 // by original id: index among the long rows, -1 otherwise
+    DBuf<int32_t> long_orig;              // long rows, original ids
+    DBuf<double> part_long;               // fronts x long rows: sweep partials
     int32_t n_long = 0;
     int64_t max_long = 0, long_chunks = 0;
     DBuf<double> long_part;  // chunk results of the long-row scans
@@ -638,7 +646,8 @@ int sync_and_verify(uno_kkt_t h) {
         }
         {
             TimerScope t2(h, KC_ROWSUM);
-            HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
+            if (h->use_front_sweeps) HIPCHK(h, launch_rowsum_norm_orig(h->scan, h->rowsum.p, h->stream));
+            else HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
         }
         HIPCHK(h, hipMemcpyAsync(h->h_counters + 9, h->anorm.p, 8, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -913,6 +922,29 @@ int upload_structure(uno_kkt_t h) {
     hipStream_t s = h->stream;
     HIPCHK(h, S.identity_dups ? (h->dup_ptr.release(), hipSuccess) : h->dup_ptr.upload(S.dup_ptr, s));
     HIPCHK(h, h->dup_pos.upload(S.dup_pos, s));
+    if (S.identity_dups) {
+        h->slot_src.release();
+    } else {
+        // multi_slots: per slot with several COO positions {slot, p0, p1, p2} (-1 padded), or {slot, -2 - q0,
+        // count, 0} (dup_pos[q0 ..]) for more than three
+        std::vector<int32_t> src((size_t)S.nu), multi;
+        for (int64_t e = 0; e < S.nu; ++e) {
+            const int32_t q0 = S.dup_ptr[e], cnt = S.dup_ptr[e + 1] - q0;
+            src[e] = cnt == 1 ? S.dup_pos[q0] : -1;
+            if (cnt == 1) continue;
+            multi.push_back((int32_t)e);
+            if (cnt <= 3) {
+                for (int t = 0; t < 3; ++t) multi.push_back(t < cnt ? S.dup_pos[q0 + t] : -1);
+            } else {
+                multi.push_back(-2 - q0);
+                multi.push_back(cnt);
+                multi.push_back(0);
+            }
+        }
+        HIPCHK(h, h->slot_src.upload(src, s));
+        HIPCHK(h, h->multi_slots.upload(multi, s));
+        h->n_multi = (int64_t)multi.size() / 4;
+    }
     HIPCHK(h, h->ent_r.upload(S.ent_r, s));
     HIPCHK(h, h->ent_c.upload(S.ent_c, s));
     HIPCHK(h, h->ent_lpos.upload(S.ent_lpos, s));
@@ -950,7 +982,8 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->cptr.upload(S.cptr, s));
     HIPCHK(h, h->rptr.upload(S.rptr, s));
     HIPCHK(h, h->rslot.upload(S.rslot, s));
-    if (h->world == 1) {
+    h->use_front_sweeps = h->world == 1 && h->front_sweeps && S.max_m <= kMaxSweepFront;
+    if (h->world == 1 && !h->use_front_sweeps) {
         HIPCHK(h, h->rowpartner.upload(S.rowpartner, s));
         HIPCHK(h, h->uvalR.alloc(S.rowpartner.size()));
     }
@@ -966,6 +999,25 @@ int upload_structure(uno_kkt_t h) {
         }
         h->n_long = (int32_t)lr.size();
         HIPCHK(h, h->long_rows.upload(lr, s));
+        if (h->use_front_sweeps) {
+            std::vector<int8_t> lp((size_t)std::max<int64_t>(n, 1), (int8_t)-1);
+            std::vector<int32_t> lo(lr.size());
+            for (size_t k = 0; k < lr.size(); ++k) {
+                lo[k] = S.perm[lr[k]];
+                lp[lo[k]] = (int8_t)k;
+            }
+            if (lr.size() > 127) h->use_front_sweeps = false;  // int8 index
+            HIPCHK(h, h->longpos.upload(lp, s));
+            HIPCHK(h, h->long_orig.upload(lo, s));
+            const int64_t npl = std::max<int64_t>((int64_t)S.nf * (int64_t)lr.size(), 1);
+            HIPCHK(h, h->part_long.alloc(npl));
+            // fronts without a given long row never write its partial: those slots stay 0
+            HIPCHK(h, hipMemsetAsync(h->part_long.p, 0, sizeof(double) * npl, s));
+            if (!h->use_front_sweeps) {  // more than 127 dense rows: the row-major sweeps
+                HIPCHK(h, h->rowpartner.upload(S.rowpartner, s));
+                HIPCHK(h, h->uvalR.alloc(S.rowpartner.size()));
+            }
+        }
         h->long_chunks = (h->max_long + kLongChunk - 1) / kLongChunk;
         HIPCHK(h, h->long_part.alloc(std::max<int64_t>((int64_t)h->n_long * h->long_chunks, 1)));
         HIPCHK(h, h->long_cnt.alloc(std::max<int64_t>(h->n_long, 1)));
@@ -1038,13 +1090,16 @@ int enqueue_factorization(uno_kkt_t h) {
     hipStream_t s = h->stream;
     HIPCHK(h, hipMemsetAsync(h->counters.p, 0, 8 * sizeof(unsigned long long), s));
     HIPCHK(h, hipMemsetAsync(h->anorm.p, 0, sizeof(unsigned long long), s));
-    {
+    if (h->use_front_sweeps) {
+        // k_pack runs inside launch_front_sweeps (timed with the scaling)
+    } else {
         TimerScope t(h, KC_PACK);
         if (h->world == 1) {
-            HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, 0, S.nu, h->uval.p, s));
+            HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->slot_src.p, 0, S.nu, h->uval.p, s));
+            if (h->slot_src.p) HIPCHK(h, launch_pack_multi(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->multi_slots.p, h->n_multi, h->uval.p, s));
         } else {
             for (const auto& r : h->dist.pack_ranges)
-                HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, r.first, r.second, h->uval.p, s));
+                HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, nullptr, r.first, r.second, h->uval.p, s));
         }
     }
     {
@@ -1059,7 +1114,23 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.scale_in = h->w.p;      // (free until the solve)
         h->scan = SA;
         h->norm_valid = false;
-        if (h->world == 1 && h->overlap_norm && !h->exact_next) {
+        if (h->use_front_sweeps) {
+            SweepArgs W;
+            W.nf = S.nf; W.n = S.n; W.fm = h->fm.p; W.rows_off = h->rows_off.p; W.rows = h->rows.p;
+            W.ent_off = h->ent_off.p; W.ent_lpos = h->ent_lpos.p; W.values = h->values_ptr; W.dup_ptr = h->dup_ptr.p;
+            W.dup_pos = h->dup_pos.p; W.slot_src = h->slot_src.p; W.uval = h->uval.p;
+            W.multi = h->multi_slots.p; W.n_multi = h->n_multi; W.scale = h->scale.p; W.ent_total = S.nu;
+            W.rmax = reinterpret_cast<unsigned long long*>(h->rmax.p); W.longpos = h->longpos.p;
+            W.long_orig = h->long_orig.p; W.n_long = h->n_long; W.part_long = h->part_long.p; W.max_m = (int)S.max_m;
+            HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
+            if (h->overlap_norm && !h->exact_next) {
+                h->last_optimistic = true;  // row sums only if a pivot is small (sync_and_verify)
+            } else {
+                HIPCHK(h, launch_rowsum_norm_orig(SA, h->rowsum.p, s));
+                h->last_optimistic = false;
+                h->norm_valid = true;
+            }
+        } else if (h->world == 1 && h->overlap_norm && !h->exact_next) {
             // threshold 0 and a record of the smallest accepted pivot; the row sums only if it is small
             // (sync_and_verify)
             HIPCHK(h, launch_scale_sweeps(SA, h->scale_iters, h->rmax.p, s));
@@ -1244,6 +1315,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "pin_host_values") h->pin_host = value != 0.0;
     else if (n == "mfma_fronts") h->mfma_fronts = value != 0.0;
+    else if (n == "front_sweeps") h->front_sweeps = value != 0.0;
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
     else if (n == "gather_solution") h->gather_solution = value != 0.0;
@@ -1671,7 +1743,8 @@ int uno_kkt_debug_scaling(uno_kkt_t h, double* scale, double* anorm) {
     if (!h->factored && h->st.factorizations == 0) return set_err(h, UNO_KKT_ERR_STATE, "no factorization");
     HIPCHK(h, hipSetDevice(h->device));
     if (h->world == 1 && !h->norm_valid && h->scan.n > 0) {  // skipped by the bound: compute it now
-        HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
+        if (h->use_front_sweeps) HIPCHK(h, launch_rowsum_norm_orig(h->scan, h->rowsum.p, h->stream));
+        else HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         h->norm_valid = true;
     }
@@ -1793,7 +1866,8 @@ int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* 
         if (rc != UNO_KKT_OK) return rc;
     }
     if (!h->packed_valid) {
-        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, 0, S.nu, h->uval.p, s));
+        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->slot_src.p, 0, S.nu, h->uval.p, s));
+        if (h->slot_src.p) HIPCHK(h, launch_pack_multi(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->multi_slots.p, h->n_multi, h->uval.p, s));
         h->packed_valid = true;
     }
     SymvArgs A;

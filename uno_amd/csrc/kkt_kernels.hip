@@ -35,17 +35,42 @@ __device__ __forceinline__ unsigned long long as_bits(double d) { return (unsign
 // pack + scaling
 // ------------------------------------------------------------------------------------------------
 
+// slot_src (duplicates present): the slot's single COO position, or < 0 for a slot with several, which
+// k_pack_multi writes from its list (dup_ptr range summed in ascending COO position): the slots of one
+// COO position take two dependent loads, and no wave waits for the duplicates' longer chain
 __global__ void k_pack(const double* __restrict__ values, const int32_t* __restrict__ dup_ptr,
-                       const int32_t* __restrict__ dup_pos, int64_t begin, int64_t end, double* __restrict__ uval) {
+                       const int32_t* __restrict__ dup_pos, const int32_t* __restrict__ slot_src, int64_t begin,
+                       int64_t end, double* __restrict__ uval) {
     for (int64_t s = begin + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < end; s += (int64_t)gridDim.x * blockDim.x) {
-        double v;
         if (dup_ptr == nullptr) {
-            v = values[dup_pos[s]];
+            uval[s] = values[dup_pos[s]];
+        } else if (slot_src != nullptr) {
+            const int32_t src = slot_src[s];
+            if (src >= 0) uval[s] = 0.0 + values[src];  // as the summed form: -0.0 packs as +0.0
         } else {
-            v = 0.0;  // duplicates summed in ascending COO position (oracle order)
+            double v = 0.0;  // duplicates summed in ascending COO position (oracle order)
             for (int32_t q = dup_ptr[s]; q < dup_ptr[s + 1]; ++q) v += values[dup_pos[q]];
+            uval[s] = v;
         }
-        uval[s] = v;
+    }
+}
+
+// multi: per slot {slot, p0, p1, p2} (COO positions ascending, -1 padded) or {slot, -2 - q0, count, 0}
+__global__ void k_pack_multi(const double* __restrict__ values, const int32_t* __restrict__ dup_ptr,
+                             const int32_t* __restrict__ dup_pos, const int32_t* __restrict__ multi, int64_t count,
+                             double* __restrict__ uval) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < count; t += (int64_t)gridDim.x * blockDim.x) {
+        const int4 d = reinterpret_cast<const int4*>(multi)[t];
+        double v = 0.0;  // duplicates summed in ascending COO position (oracle order)
+        if (d.y >= -1) {
+            const double a = values[d.y], b = d.z >= 0 ? values[d.z] : 0.0, c = d.w >= 0 ? values[d.w] : 0.0;
+            v += a;
+            if (d.z >= 0) v += b;
+            if (d.w >= 0) v += c;
+        } else {
+            for (int32_t q = -2 - d.y; q < -2 - d.y + d.z; ++q) v += values[dup_pos[q]];
+        }
+        uval[d.x] = v;
     }
 }
 
@@ -412,6 +437,111 @@ __global__ __launch_bounds__(256) void k_rowscanR(ScanArgs A) {
         acc = MODE == 2 ? acc + o : fmax(acc, o);
     }
     if (lane == 0) rowR_write<MODE>(A, i, acc, si);
+}
+
+// ---- single-GPU equilibration on the fronts' slots (SweepArgs) ----
+// Every entry of the lower triangle is one packed slot of exactly one front, and both its rows are in
+// that front's row list, so a row's maximum is the maximum over the fronts holding it of the front's
+// partial.  One wave per front: the entries' |s_r a s_c| (the oracle's multiplication order, s of the
+// larger original id first: bit-identical to oracle/kkt_oracle.c) reduce into the front's rows in LDS
+// (64-bit max on the bit patterns: order-free), then one atomic max per (front, row) into rmax.  The
+// first sweep (FIRST: s = 1) runs right after k_pack.
+template <bool FIRST>
+__global__ __launch_bounds__(64) void k_sweep_front(SweepArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double swm[];
+    const int f = blockIdx.x;
+    const int m = A.fm[f];
+    const int lane = threadIdx.x;
+    double* sl = swm;                                                         // m: the front rows' scaling
+    unsigned long long* rm = reinterpret_cast<unsigned long long*>(swm + m);  // m: row maxima (bits)
+    const int64_t ro = A.rows_off[f];
+    const int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    // Each lane takes EB consecutive slots: slots are ordered by (column, row), so a lane's slots mostly
+    // share a column and the column maximum is kept in a register, flushed to LDS when the column
+    // changes (one LDS atomic per run instead of one per slot on a single, conflicting address).
+    constexpr int EB = 8;
+    uint32_t lp[EB];
+    double v[EB];
+    auto load = [&](int64_t eb) {
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            const int64_t e = eb + u;
+            const bool ok = e < e1;
+            lp[u] = ok ? A.ent_lpos[e] : 0xffffffffu;
+            v[u] = ok ? A.uval[e] : 0.0;
+        }
+    };
+    load(e0 + (int64_t)lane * EB);  // the first batch is in flight while the rows' scalings are gathered
+    for (int q = lane; q < m; q += 64) {
+        rm[q] = 0ull;
+        if (!FIRST) sl[q] = A.scale[A.rows[ro + q]];
+    }
+    __syncthreads();
+    for (int64_t base = e0;;) {
+        int cc = -1;
+        unsigned long long cm = 0ull;
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            if (lp[u] == 0xffffffffu) break;  // beyond the slot range (the rest of the lane's chunk too)
+            const int lr = (int)(lp[u] >> 16), lc = (int)(lp[u] & 0x7fffu);
+            double w = fabs(v[u]);
+            if (!FIRST) {
+                const double sr = sl[lr], sc = sl[lc];
+                w = (lp[u] & 0x8000u) ? sc * w * sr : sr * w * sc;
+            }
+            const unsigned long long bw = as_bits(w);
+            atomicMax(rm + lr, bw);
+            if (lc != cc) {
+                if (cc >= 0) atomicMax(rm + cc, cm);
+                cc = lc;
+                cm = bw;
+            } else {
+                cm = cm > bw ? cm : bw;
+            }
+        }
+        if (cc >= 0) atomicMax(rm + cc, cm);
+        base += (int64_t)EB * 64;
+        if (base >= e1) break;  // uniform
+        load(base + (int64_t)lane * EB);
+    }
+    __syncthreads();
+    for (int q = lane; q < m; q += 64) {
+        const int32_t r = A.rows[ro + q];
+        const unsigned long long bw = rm[q];
+        const int k = A.n_long > 0 ? (int)A.longpos[r] : -1;
+        if (k >= 0) A.part_long[(int64_t)f * A.n_long + k] = as_double(bw);  // every front writes its slot
+        else if (bw != 0ull) atomicMax(A.rmax + r, bw);
+    }
+}
+
+// long (dense) rows: thread t of the grid reduces fronts t, t + grid, ... (their n_long partials are
+// contiguous) into the block's LDS maxima, then one atomic max per (block, long row) -- max is
+// order-free, so the result is the same in every run
+__global__ __launch_bounds__(256) void k_sweep_long_fin(SweepArgs A) {
+    extern __shared__ unsigned long long lred[];
+    for (int k = threadIdx.x; k < A.n_long; k += 256) lred[k] = 0ull;
+    __syncthreads();
+    const int64_t stride = (int64_t)gridDim.x * 256;
+    for (int k = 0; k < A.n_long; ++k) {
+        double mx = 0.0;
+        for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < A.nf; f += stride) mx = fmax(mx, A.part_long[f * A.n_long + k]);
+        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+        if ((threadIdx.x & 63) == 0 && mx > 0.0) atomicMax(lred + k, as_bits(mx));
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < A.n_long; k += 256)
+        if (lred[k] != 0ull) atomicMax(A.rmax + A.long_orig[k], lred[k]);
+}
+
+// s <- s / sqrt(r) (s = 1 before the first sweep; rows without entries keep s), and r <- 0 for the next sweep
+__global__ void k_sweep_update(unsigned long long* __restrict__ rmax, double* __restrict__ scale, int64_t n, int first) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const double r = as_double(rmax[i]);
+        double sc = first ? 1.0 : scale[i];
+        if (r > 0.0) sc = sc / sqrt(r);
+        scale[i] = sc;
+        rmax[i] = 0ull;
+    }
 }
 
 // scaling by original id for the factorization / solve kernels: scale[perm[i]] = scaleN[i]
@@ -2884,10 +3014,17 @@ static int grid_for(int64_t n, int block) {
     return (int)g;
 }
 
-hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t begin, int64_t end,
-                       double* uval, hipStream_t s) {
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* slot_src,
+                       int64_t begin, int64_t end, double* uval, hipStream_t s) {
     if (end <= begin) return hipSuccess;
-    hipLaunchKernelGGL(k_pack, dim3(grid_for(end - begin, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, begin, end, uval);
+    hipLaunchKernelGGL(k_pack, dim3(grid_for(end - begin, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, slot_src, begin, end, uval);
+    return hipGetLastError();
+}
+
+hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
+                             int64_t count, double* uval, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_pack_multi, dim3(grid_for(count, 256)), dim3(256), 0, s, values, dup_ptr, dup_pos, multi, count, uval);
     return hipGetLastError();
 }
 
@@ -2991,6 +3128,42 @@ static hipError_t launch_rowscanR(const ScanArgs& A, hipStream_t s) {
 // iters sweeps over the row-major copy.  The scalings live in the new numbering in A.scale_in / A.scale_out
 // (two scratch buffers of n doubles, the last sweep writes A.scale_out); A.scale (by original id) receives
 // the final one.
+hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s) {
+    if (A.n == 0) return hipSuccess;
+    const size_t sh = 16 * (size_t)std::max(A.max_m, 1);
+    const dim3 gn(grid_for(A.n, 256));
+    hipError_t e = hipMemsetAsync(A.rmax, 0, sizeof(unsigned long long) * A.n, s);
+    if (e != hipSuccess) return e;
+    if (A.nf > 0) {  // COO values -> packed slots (duplicates summed)
+        e = launch_pack(A.values, A.dup_ptr, A.dup_pos, A.slot_src, 0, A.ent_total, A.uval, s);
+        if (e != hipSuccess) return e;
+        if (A.slot_src != nullptr) e = launch_pack_multi(A.values, A.dup_ptr, A.dup_pos, A.multi, A.n_multi, A.uval, s);
+        if (e != hipSuccess) return e;
+    }
+    for (int it = 0; it < (iters > 0 ? iters : 1); ++it) {
+        if (A.nf > 0) {
+            if (it == 0) hipLaunchKernelGGL(k_sweep_front<true>, dim3((unsigned)A.nf), dim3(64), sh, s, A);
+            else hipLaunchKernelGGL(k_sweep_front<false>, dim3((unsigned)A.nf), dim3(64), sh, s, A);
+        }
+        if (A.n_long > 0) {
+            const unsigned gl = (unsigned)std::min<int64_t>(256, (A.nf + 255) / 256);
+            hipLaunchKernelGGL(k_sweep_long_fin, dim3(std::max(gl, 1u)), dim3(256), sizeof(unsigned long long) * A.n_long, s, A);
+        }
+        hipLaunchKernelGGL(k_sweep_update, gn, dim3(256), 0, s, A.rmax, A.scale, A.n, it == 0 ? 1 : 0);
+    }
+    if (iters == 0) hipLaunchKernelGGL(k_fill_ones, gn, dim3(256), 0, s, A.scale, A.n);  // the pass above only packed
+    return hipGetLastError();
+}
+
+hipError_t launch_rowsum_norm_orig(ScanArgs A, double* rowsum, hipStream_t s) {
+    if (A.n == 0) return hipSuccess;
+    A.out = rowsum;
+    A.list = nullptr;
+    hipError_t e = launch_rowscan(A, 2, s);
+    if (e != hipSuccess) return e;
+    return launch_normmax(rowsum, nullptr, A.n, A.anorm, s);
+}
+
 hipError_t launch_scale_sweeps(ScanArgs A, int iters, double* rmax, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     (void)rmax;

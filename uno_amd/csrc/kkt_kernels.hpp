@@ -137,6 +137,39 @@ struct ScanArgs {
 };
 constexpr int kLongRow = 2048;
 
+// single-GPU equilibration sweeps over the fronts' packed slots (k_sweep_front): row maxima of a front's
+// slots in LDS, merged over fronts with one atomic max per (front, row) -- rows longer than kLongRow
+// (dense rows, present in every front) through per-front partials instead; scalings by original id.
+struct SweepArgs {
+    int64_t nf, n;
+    const int32_t* fm;
+    const int64_t* rows_off;
+    const int32_t* rows;        // original ids
+    const int64_t* ent_off;     // nf+1 slot ranges
+    const uint32_t* ent_lpos;   // (lr << 16) | flip << 15 | lc
+    const double* values;       // caller's COO values (packed into uval by k_pack first)
+    int64_t ent_total;          // packed slots
+    const int32_t* dup_ptr;     // nullptr: one COO position per slot
+    const int32_t* dup_pos;
+    const int32_t* slot_src;    // k_pack: single COO position per slot, < 0: in `multi` (k_pack_multi)
+    const int32_t* multi;       // slots with several COO positions
+    int64_t n_multi;
+    double* uval;
+    double* scale;              // by original id
+    unsigned long long* rmax;   // n, zero between sweeps
+    const int8_t* longpos;      // by original id: index among the long rows, -1 otherwise
+    const int32_t* long_orig;   // n_long original ids
+    int32_t n_long;
+    double* part_long;          // nf * n_long
+    int max_m;
+};
+hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s);
+hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
+                             int64_t count, double* uval, hipStream_t s);
+// ||A_pre||_inf from the scaling by original id (row scans over the packed slots, no row-major copy)
+hipError_t launch_rowsum_norm_orig(ScanArgs A, double* rowsum, hipStream_t s);
+constexpr int kMaxSweepFront = 4096;  // largest front order of the front sweeps (LDS 16 B per row)
+
 // partial scans of the top (separator) rows on one rank: chunk c covers pslot[chunk_begin[c] ..
 // chunk_begin[c+1]) of top row chunk_row[c]; ppartner = original id of the slot's other index
 struct PartArgs {
@@ -156,7 +189,7 @@ struct PartArgs {
 constexpr int kLongChunk = 4096;
 
 // pack slots [begin, end)
-hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, int64_t begin, int64_t end,
+hipError_t launch_pack(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* slot_src, int64_t begin, int64_t end,
                        double* uval, hipStream_t s);
 // single-GPU equilibration: `iters` max-scaling sweeps over all rows, then row sums and ||A_pre||_inf
 hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hipStream_t s);
