@@ -398,7 +398,18 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
         // front).  Finer LDS classes ({16, 24, .., 128}) were measured slower on C3 (2.36 vs 1.99 ms):
         // the one-wave kernel is VALU-issue bound at levels 0-1 and more co-resident fronts per CU
         // only lengthen every front; a class smaller than kMinClass absorbs the next smaller one.
-        static const int caps[] = {32, 64, kMaxWaveFront, 128};
+        static const std::vector<int> caps = [] {  // UNO_KKT_CAPS="32,48,64,72,128" (experiments)
+            std::vector<int> c{32, 64, kMaxWaveFront, 128};
+            if (const char* e = getenv("UNO_KKT_CAPS")) {
+                c.clear();
+                for (const char* p = e; *p;) {
+                    c.push_back(atoi(p));
+                    while (*p && *p != ',') ++p;
+                    if (*p) ++p;
+                }
+            }
+            return c;
+        }();
         constexpr int kMinClass = 2048;
         auto prev_cap = [](int c) {
             int pc = 0;
