@@ -16,6 +16,7 @@
 #ifndef UNO_KKT_H
 #define UNO_KKT_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -176,6 +177,23 @@ typedef struct uno_kkt_group* uno_kkt_group_t;
 int uno_kkt_group_create(uno_kkt_group_t* group, int world);
 void uno_kkt_group_destroy(uno_kkt_group_t group);
 int uno_kkt_attach_local(uno_kkt_t handle, uno_kkt_group_t group, int rank);
+
+/* Host-staged transport: the caller's own exchange on HOST buffers (e.g. MPI, or torch.distributed over
+ * gloo), for one process per rank where RCCL is not available (several ranks on one GPU).  Device data
+ * is staged through page-locked buffers.  send / recv post an operation on a host buffer that stays
+ * valid until the next group_end call, which completes every operation posted since the previous one
+ * (the library calls group_end after each batch, and right after a send / recv outside a batch).
+ * allreduce reduces `count` 8-byte elements in place (op 0: sum u64, 1: max u64, 2: max f64, 3: sum
+ * f64), broadcast copies `bytes` from `root` in place; both block.  Callbacks return 0 on success. */
+typedef struct {
+    void* ctx;
+    int (*send)(void* ctx, const void* buf, size_t bytes, int peer);
+    int (*recv)(void* ctx, void* buf, size_t bytes, int peer);
+    int (*group_end)(void* ctx);
+    int (*allreduce)(void* ctx, void* buf, size_t count, int op);
+    int (*broadcast)(void* ctx, void* buf, size_t bytes, int root);
+} uno_kkt_host_comm_t;
+int uno_kkt_attach_host(uno_kkt_t handle, const uno_kkt_host_comm_t* comm, int rank, int world);
 
 typedef struct {
     int64_t rank, world;

@@ -172,7 +172,97 @@ private:
     int r_, w_;
 };
 
+// ------------------------------------------------------------------------------------------------
+// host-staged (caller's callbacks on host buffers)
+// ------------------------------------------------------------------------------------------------
+class HostTransport final : public Transport {
+public:
+    HostTransport(const HostComm& cb, int r, int w) : cb_(cb), r_(r), w_(w) {}
+    ~HostTransport() override {
+        for (auto& p : pend_) hipHostFree(p.host);
+    }
+    int rank() const override { return r_; }
+    int size() const override { return w_; }
+    std::string describe() const override { return "host-staged(" + std::to_string(w_) + " ranks)"; }
+    hipError_t group_begin() override {
+        in_group_ = true;
+        return hipSuccess;
+    }
+    hipError_t group_end() override {
+        in_group_ = false;
+        return complete();
+    }
+    hipError_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+        if (bytes == 0) return hipSuccess;
+        void* hb = nullptr;
+        hipError_t e = stage(bytes, &hb);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(hb, buf, bytes, hipMemcpyDeviceToHost);
+        pend_.push_back({hb, nullptr, 0});
+        if (e == hipSuccess && cb_.send(cb_.ctx, hb, bytes, peer) != 0) e = hipErrorLaunchFailure;
+        return (e != hipSuccess || in_group_) ? e : complete();
+    }
+    hipError_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+        if (bytes == 0) return hipSuccess;
+        void* hb = nullptr;
+        hipError_t e = stage(bytes, &hb);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);  // earlier work on `buf` is done before it is overwritten
+        pend_.push_back({hb, buf, bytes});
+        if (e == hipSuccess && cb_.recv(cb_.ctx, hb, bytes, peer) != 0) e = hipErrorLaunchFailure;
+        return (e != hipSuccess || in_group_) ? e : complete();
+    }
+    hipError_t allreduce(void* buf, size_t count, RedOp op, hipStream_t s) override {
+        if (count == 0) return hipSuccess;
+        void* hb = nullptr;
+        hipError_t e = stage(count * 8, &hb);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess) e = hipMemcpy(hb, buf, count * 8, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && cb_.allreduce(cb_.ctx, hb, count, (int)op) != 0) e = hipErrorLaunchFailure;
+        if (e == hipSuccess) e = hipMemcpy(buf, hb, count * 8, hipMemcpyHostToDevice);
+        hipHostFree(hb);
+        return e;
+    }
+    hipError_t broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+        if (bytes == 0) return hipSuccess;
+        void* hb = nullptr;
+        hipError_t e = stage(bytes, &hb);
+        if (e == hipSuccess) e = hipStreamSynchronize(s);
+        if (e == hipSuccess && r_ == root) e = hipMemcpy(hb, buf, bytes, hipMemcpyDeviceToHost);
+        if (e == hipSuccess && cb_.broadcast(cb_.ctx, hb, bytes, root) != 0) e = hipErrorLaunchFailure;
+        if (e == hipSuccess && r_ != root) e = hipMemcpy(buf, hb, bytes, hipMemcpyHostToDevice);
+        hipHostFree(hb);
+        return e;
+    }
+
+private:
+    struct Pending {
+        void* host;
+        void* dev;  // receives: destination, copied after the exchange completes
+        size_t bytes;
+    };
+    static hipError_t stage(size_t bytes, void** hb) { return hipHostMalloc(hb, bytes, hipHostMallocDefault); }
+    // every posted send / receive is finished by the caller, then received data goes to the device
+    hipError_t complete() {
+        hipError_t e = cb_.group_end(cb_.ctx) == 0 ? hipSuccess : hipErrorLaunchFailure;
+        for (auto& p : pend_) {
+            if (e == hipSuccess && p.dev) e = hipMemcpy(p.dev, p.host, p.bytes, hipMemcpyHostToDevice);
+            hipHostFree(p.host);
+        }
+        pend_.clear();
+        return e;
+    }
+    HostComm cb_;
+    int r_, w_;
+    bool in_group_ = false;
+    std::vector<Pending> pend_;
+};
+
 }  // namespace
+
+Transport* make_host_transport(const HostComm& cb, int rank, int world) {
+    if (!cb.send || !cb.recv || !cb.group_end || !cb.allreduce || !cb.broadcast || rank < 0 || rank >= world) return nullptr;
+    return new HostTransport(cb, rank, world);
+}
 
 Transport* make_local_transport(LocalGroup* g, int rank) {
     if (!g || rank < 0 || rank >= g->world) return nullptr;

@@ -4,10 +4,12 @@
 // exchanges are the contribution blocks (factor) and update vectors (forward solve) of the subtree
 // roots, sent to the rank that owns the top of the assembly tree, the broadcast of the top rows of
 // the solution (backward solve), and small reductions (equilibration of the separator rows, the
-// null-pivot norm, inertia counters).  Two implementations:
+// null-pivot norm, inertia counters).  Three implementations:
 //   RcclTransport  -- one process per GPU, RCCL point-to-point + collectives over xGMI;
 //   LocalTransport -- several handles in one process (threads), device-to-device copies; used to run
-//                     and test the distributed algorithm on a single GPU.
+//                     and test the distributed algorithm on a single GPU;
+//   HostTransport  -- one process per rank, the caller's host-side exchange (callbacks) through
+//                     page-locked staging buffers.
 // The reference has no multi-process path (MUMPS par=1, MUMPSSolver.cpp:17); this is new.
 #pragma once
 
@@ -44,6 +46,20 @@ struct LocalGroup;
 LocalGroup* local_group_create(int world);
 void local_group_destroy(LocalGroup* g);
 Transport* make_local_transport(LocalGroup* g, int rank);
+
+// Host-staged: the caller's exchange on host buffers (callbacks, e.g. torch.distributed over gloo or
+// MPI); device data goes through page-locked staging buffers.  For one process per rank when RCCL is
+// not available (several ranks on one GPU: RCCL refuses duplicate devices), and for tests of the
+// multi-process orchestration.
+struct HostComm {
+    void* ctx;
+    int (*send)(void* ctx, const void* buf, size_t bytes, int peer);
+    int (*recv)(void* ctx, void* buf, size_t bytes, int peer);
+    int (*group_end)(void* ctx);
+    int (*allreduce)(void* ctx, void* buf, size_t count, int op);
+    int (*broadcast)(void* ctx, void* buf, size_t bytes, int root);
+};
+Transport* make_host_transport(const HostComm& cb, int rank, int world);
 
 // RCCL: unique id from rank 0 (NCCL_UNIQUE_ID_BYTES = 128), then every rank attaches with it.
 int rccl_unique_id(unsigned char out[128]);

@@ -1957,6 +1957,14 @@ int uno_kkt_attach_local(uno_kkt_t h, uno_kkt_group_t g, int rank) {
     return attach(h, t);
 }
 
+int uno_kkt_attach_host(uno_kkt_t h, const uno_kkt_host_comm_t* comm, int rank, int world) {
+    if (!h || !comm) return UNO_KKT_ERR_ARG;
+    ukkt::HostComm cb{comm->ctx, comm->send, comm->recv, comm->group_end, comm->allreduce, comm->broadcast};
+    ukkt::Transport* t = ukkt::make_host_transport(cb, rank, world);
+    if (!t) return set_err(h, UNO_KKT_ERR_ARG, "incomplete host transport or bad rank");
+    return attach(h, t);
+}
+
 int uno_kkt_dist_info(uno_kkt_t h, uno_kkt_dist_info_t* out) {
     if (!h || !out) return UNO_KKT_ERR_ARG;
     memset(out, 0, sizeof(*out));

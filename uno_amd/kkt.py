@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = [
     "uno_kkt_version", "uno_kkt_comm_unique_id", "uno_kkt_attach_rccl", "uno_kkt_group_create",
     "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info", "uno_kkt_rhs_setup",
     "uno_kkt_assemble_rhs", "uno_kkt_assemble_direction", "uno_kkt_symv", "uno_kkt_quadratic_product",
-    "uno_kkt_barrier_setup", "uno_kkt_barrier_count", "uno_kkt_assemble_barrier",
+    "uno_kkt_barrier_setup", "uno_kkt_barrier_count", "uno_kkt_assemble_barrier", "uno_kkt_attach_host",
 ]
 
 
@@ -99,6 +99,7 @@ def load_library():
     lib.uno_kkt_group_destroy.restype = None
     lib.uno_kkt_attach_local.argtypes = [vp, vp, ctypes.c_int]
     lib.uno_kkt_dist_info.argtypes = [vp, ctypes.POINTER(KKTDistInfo)]
+    lib.uno_kkt_attach_host.argtypes = [vp, ctypes.POINTER(HostCommStruct), ctypes.c_int, ctypes.c_int]
     lib.uno_kkt_debug_scaling.argtypes = [vp, _f64p, _f64p]
     lib.uno_kkt_barrier_setup.argtypes = [vp, ctypes.c_int64, _f64p, _f64p]
     lib.uno_kkt_barrier_count.argtypes = [vp]
@@ -284,6 +285,11 @@ class HipKKT:
     def attach_local(self, group, rank):
         self._check(self.lib.uno_kkt_attach_local(self.h, group.g, int(rank)))
 
+    def attach_host(self, comm, rank, world):
+        """Host-staged transport (uno_kkt_attach_host) driven by `comm` (e.g. GlooComm); one process per rank."""
+        self._host_comm = comm  # the callbacks must outlive the handle
+        self._check(self.lib.uno_kkt_attach_host(self.h, ctypes.byref(comm.struct), int(rank), int(world)))
+
     def dist_info(self):
         d = KKTDistInfo()
         self._check(self.lib.uno_kkt_dist_info(self.h, ctypes.byref(d)))
@@ -298,6 +304,68 @@ def rccl_unique_id():
     if rc != UNO_KKT_OK:
         raise KKTError(rc, "ncclGetUniqueId failed")
     return buf.raw
+
+
+_CB_SEND = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int)
+_CB_GROUP_END = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p)
+
+
+class HostCommStruct(ctypes.Structure):
+    """uno_kkt_host_comm_t (include/uno_kkt.h)"""
+    _fields_ = [("ctx", ctypes.c_void_p), ("send", _CB_SEND), ("recv", _CB_SEND), ("group_end", _CB_GROUP_END),
+                ("allreduce", _CB_SEND), ("broadcast", _CB_SEND)]
+
+
+class GlooComm:
+    """Host-staged exchange of uno_kkt_attach_host over torch.distributed (gloo backend, an initialised
+    default group): send / recv post isend / irecv on the staged host buffer, group_end waits for them,
+    allreduce / broadcast are the blocking collectives (8-byte elements; u64 values are bit patterns of
+    non-negative doubles or counters, below 2^63, so int64 arithmetic is exact)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist, self.group, self.pending = torch, dist, group, []
+
+        def view(buf, nbytes, dtype):
+            raw = (ctypes.c_uint8 * nbytes).from_address(buf)
+            return torch.frombuffer(raw, dtype=dtype)
+
+        def guard(fn):
+            def run(*a):
+                try:
+                    fn(*a)
+                    return 0
+                except Exception as e:  # noqa: BLE001 -- reported to the library as a failed exchange
+                    import sys
+                    print(f"[GlooComm] {e!r}", file=sys.stderr)
+                    return -1
+            return run
+
+        def send(ctx, buf, nbytes, peer):
+            t = view(buf, nbytes, torch.uint8)
+            self.pending.append((dist.isend(t, int(peer), group=self.group), t))
+
+        def recv(ctx, buf, nbytes, peer):
+            t = view(buf, nbytes, torch.uint8)
+            self.pending.append((dist.irecv(t, int(peer), group=self.group), t))
+
+        def group_end(ctx):
+            for w, _ in self.pending:
+                w.wait()
+            self.pending.clear()
+
+        def allreduce(ctx, buf, count, op):
+            t = view(buf, 8 * count, torch.int64 if op in (0, 1) else torch.float64)
+            ro = dist.ReduceOp.SUM if op in (0, 3) else dist.ReduceOp.MAX
+            dist.all_reduce(t, op=ro, group=self.group)
+
+        def broadcast(ctx, buf, nbytes, root):
+            dist.broadcast(view(buf, nbytes, torch.uint8), int(root), group=self.group)
+
+        self._cbs = (_CB_SEND(guard(send)), _CB_SEND(guard(recv)), _CB_GROUP_END(guard(group_end)),
+                     _CB_SEND(guard(allreduce)), _CB_SEND(guard(broadcast)))
+        self.struct = HostCommStruct(None, *self._cbs)
 
 
 class LocalGroup:
