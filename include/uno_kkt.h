@@ -69,7 +69,9 @@ void uno_kkt_destroy(uno_kkt_t handle);
  * "null_tol_factor" (default 1e-5: thres = eps*1e-5*||A_pre||_inf, ICNTL(24)=1 with CNTL(3)=0),
  * "scale_iters" (default 3, ICNTL(8)=8 restated as symmetric
  * infinity-norm sweeps; the oracle uses the same default), "leaf_size" (ND leaf, default 32),
- * "max_block" (max supernode width, default 64), "timing" (1 = per-kernel HIP event timing),
+ * "max_block" (max supernode width, default 64), "wide_group" / "wide_block" (a separator or dense-row
+ * group longer than wide_group = 128 columns is cut into supernodes of up to wide_block = 4096 columns,
+ * factored as large fronts), "timing" (1 = per-kernel HIP event timing),
  * "delay_relaxed" (default 1: a front whose fully-summed block has no pivot passing u is amalgamated
  * into its parent and refactored -- the delayed-pivot rule of MUMPS; 0 = accept relaxed pivots). */
 int uno_kkt_set_option(uno_kkt_t handle, const char* name, double value);

@@ -249,12 +249,13 @@ std::string order_pattern(int64_t n, int64_t nnz, const int64_t* row, const int6
     group_start.push_back(N);
     P.perm.swap(order);
 
-    // ---- supernodes: each group cut into blocks of at most max_block columns ----
+    // ---- supernodes: each group cut into blocks of at most max_block (long groups: wide_block) columns ----
     for (size_t gi = 0; gi + 1 < group_start.size(); ++gi) {
         int32_t s = group_start[gi], e = group_start[gi + 1];
         int32_t len = e - s;
         if (len <= 0) continue;
-        int32_t nb = (len + opt.max_block - 1) / opt.max_block;
+        const int32_t wmax = len > opt.wide_group ? std::max(opt.max_block, opt.wide_block) : opt.max_block;
+        int32_t nb = (len + wmax - 1) / wmax;
         for (int32_t b = 0; b < nb; ++b) P.bfirst.push_back(s + (int32_t)((int64_t)len * b / nb));
     }
     P.bfirst.push_back(N);

@@ -18,6 +18,12 @@ namespace ukkt {
 struct AnalysisOptions {
     int leaf_size = 32;   // nested-dissection leaf (nodes)
     int max_block = 64;   // widest supernode (fully-summed columns per front)
+    // a group (separator / dense rows) longer than wide_group columns has fronts beyond the LDS kernels
+    // anyway: it is cut into blocks of at most wide_block columns instead of max_block, so the large-front
+    // path factors it as one front in panels instead of a chain of max_block-column fronts, each copying
+    // the whole remaining group as its contribution block
+    int wide_group = 128;
+    int wide_block = 4096;
     double dense_factor = 10.0;  // dense node: degree > max(16, dense_factor * sqrt(n))
 };
 

@@ -57,6 +57,7 @@ struct Launch {
     int begin, count, mmax;
     bool global;
     int level;
+    int pmax = 0, maxch = 0;  // large fronts: widest panel sequence, most children (assembly passes)
 };
 
 // one solve launch: fronts solve_fronts[begin, begin+count) of one level; wave kernels (p <= 64,
@@ -157,6 +158,8 @@ struct uno_kkt {
     int front_sweeps = 1;                 // option front_sweeps: equilibration over the fronts' slots (k_sweep_front)
     bool use_front_sweeps = false;        // front_sweeps, one GPU and every front within kMaxSweepFront rows
     DBuf<int8_t> longpos;                 // by original id: index among the long rows, -1 otherwise
+    DBuf<int32_t> sweep_big;              // fronts of more than kSweepBigSlots slots (sliced sweeps)
+    int32_t n_sweep_big = 0, sweep_slices = 1;
     DBuf<int32_t> long_orig;              // long rows, original ids
     DBuf<double> part_long;               // fronts x long rows: sweep partials
     int32_t n_long = 0;
@@ -292,13 +295,15 @@ int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* 
 // Fronts beyond LDS (m > kMaxLdsFront): blocked factorization in HBM scratch (kkt_kernels.hip k_big_*).
 // Every panel + update step advances each unfinished front by at least one pivot; the host queues
 // batches of steps and checks (one small copy + stream sync per batch) until no front is left.
-int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
+int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, const Launch& L, hipStream_t s);
 
-int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
+int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, const Launch& L, hipStream_t s) {
+    const int count = L.count, mmax = L.mmax;
     if (count <= 0) return UNO_KKT_OK;
-    HIPCHK(h, launch_big_assemble(A, fronts, count, mmax, s));
-    const int nb = big_panel_width();
-    int batch = (mmax + nb - 1) / nb + 2;
+    HIPCHK(h, launch_big_assemble(A, fronts, count, mmax, L.maxch, s));
+    const int nb = big_panel_width(mmax);
+    // one panel step per nb pivots of the widest front (+2 for early panel stops before the first check)
+    int batch = (L.pmax + nb - 1) / nb + 2;
     int64_t steps = 0;
     for (;;) {
         for (int r = 0; r < batch; ++r) HIPCHK(h, launch_big_step(A, fronts, count, mmax, s));
@@ -436,7 +441,12 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
                     floor_ = prev_cap(floor_);
                 }
             }
-            P.fac.push_back({base + q, r - q, m0, global, l});
+            Launch L{base + q, r - q, m0, global, l};
+            for (int t = q; t < r; ++t) {
+                L.pmax = std::max(L.pmax, S.f_p[lv[t]]);
+                L.maxch = std::max(L.maxch, S.f_child_off[lv[t] + 1] - S.f_child_off[lv[t]]);
+            }
+            P.fac.push_back(L);
             q = r;
         }
     }
@@ -994,6 +1004,17 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->rptr.upload(S.rptr, s));
     HIPCHK(h, h->rslot.upload(S.rslot, s));
     h->use_front_sweeps = h->world == 1 && h->front_sweeps && S.max_m <= kMaxSweepFront;
+    {
+        std::vector<int32_t> big;
+        int64_t most = 0;
+        for (int32_t f = 0; f < (int32_t)S.nf; ++f) {
+            const int64_t ns = S.f_ent_off[f + 1] - S.f_ent_off[f];
+            if (ns > kSweepBigSlots) { big.push_back(f); most = std::max(most, ns); }
+        }
+        h->n_sweep_big = (int32_t)big.size();
+        h->sweep_slices = (int32_t)std::min<int64_t>(256, (most + kSweepBigSlots - 1) / kSweepBigSlots);
+        if (!big.empty()) HIPCHK(h, h->sweep_big.upload(big, s));
+    }
     if (h->world == 1 && !h->use_front_sweeps) {
         HIPCHK(h, h->rowpartner.upload(S.rowpartner, s));
         HIPCHK(h, h->uvalR.alloc(S.rowpartner.size()));
@@ -1133,6 +1154,7 @@ int enqueue_factorization(uno_kkt_t h) {
             W.multi = h->multi_slots.p; W.n_multi = h->n_multi; W.scale = h->scale.p; W.ent_total = S.nu;
             W.rmax = reinterpret_cast<unsigned long long*>(h->rmax.p); W.longpos = h->longpos.p;
             W.long_orig = h->long_orig.p; W.n_long = h->n_long; W.part_long = h->part_long.p; W.max_m = (int)S.max_m;
+            W.big_list = h->sweep_big.p; W.n_big = h->n_sweep_big; W.big_slices = h->sweep_slices;
             HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
             if (h->overlap_norm && !h->exact_next) {
                 h->last_optimistic = true;  // row sums only if a pivot is small (sync_and_verify)
@@ -1192,7 +1214,7 @@ int enqueue_factorization(uno_kkt_t h) {
             const Launch& L = lp.fac[u];
             hipStream_t ls = (u > q && h->concurrent_classes) ? h->stream3 : s;
             if (L.global) {
-                const int rc = run_big_fronts(h, A, lp.fac_fronts.p + L.begin, L.count, L.mmax, ls);
+                const int rc = run_big_fronts(h, A, lp.fac_fronts.p + L.begin, L, ls);
                 if (rc != UNO_KKT_OK) return rc;
             } else {
                 HIPCHK(h, launch_factor(A, lp.fac_fronts.p + L.begin, L.count, L.mmax, false, ls));
@@ -1224,7 +1246,7 @@ int enqueue_factorization(uno_kkt_t h) {
         for (const Launch& L : h->plan[1].fac) {
             TimerScope t(h, L.global ? KC_FACTOR_GLOBAL : KC_FACTOR_LDS);
             if (L.global) {
-                rc = run_big_fronts(h, A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, s);
+                rc = run_big_fronts(h, A, h->plan[1].fac_fronts.p + L.begin, L, s);
                 if (rc != UNO_KKT_OK) return rc;
             } else {
                 HIPCHK(h, launch_factor(A, h->plan[1].fac_fronts.p + L.begin, L.count, L.mmax, false, s));
@@ -1320,6 +1342,8 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "scale_iters") h->scale_iters = std::max(0, (int)value);
     else if (n == "leaf_size") h->aopt.leaf_size = std::max(1, (int)value);
     else if (n == "max_block") h->aopt.max_block = std::max(1, std::min((int)value, 1024));
+    else if (n == "wide_group") h->aopt.wide_group = std::max(1, (int)value);
+    else if (n == "wide_block") h->aopt.wide_block = std::max(1, std::min((int)value, 32767));
     else if (n == "dense_factor") h->aopt.dense_factor = value;
     else if (n == "timing") h->timing = value != 0.0;
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;

@@ -446,16 +446,27 @@ __global__ __launch_bounds__(256) void k_rowscanR(ScanArgs A) {
 // larger original id first: bit-identical to oracle/kkt_oracle.c) reduce into the front's rows in LDS
 // (64-bit max on the bit patterns: order-free), then one atomic max per (front, row) into rmax.  The
 // first sweep (FIRST: s = 1) runs right after k_pack.
-template <bool FIRST>
-__global__ __launch_bounds__(64) void k_sweep_front(SweepArgs A) {
+// BIG: fronts of more than kSweepBigSlots slots (the large fronts), which one wave would sweep for
+// milliseconds: grid (big fronts x slices) of 256-thread blocks, each reducing a slice of the slots into
+// its LDS row maxima, one atomic max per (block, row) straight into rmax (long rows included: there are
+// few such blocks).  The one-wave launch skips those fronts (their long-row partials stay 0).
+template <bool FIRST, bool BIG>
+__global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
     extern __shared__ __attribute__((aligned(16))) double swm[];
-    const int f = blockIdx.x;
+    const int f = BIG ? A.big_list[blockIdx.x] : blockIdx.x;
     const int m = A.fm[f];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x;  // thread of the block (one wave unless BIG)
+    const int NT = BIG ? 256 : 64;
     double* sl = swm;                                                         // m: the front rows' scaling
     unsigned long long* rm = reinterpret_cast<unsigned long long*>(swm + m);  // m: row maxima (bits)
     const int64_t ro = A.rows_off[f];
-    const int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    if (!BIG && e1 - e0 > kSweepBigSlots) return;
+    if (BIG) {
+        const int64_t chunk = ((e1 - e0 + gridDim.y - 1) / gridDim.y + 7) & ~(int64_t)7;
+        e0 += chunk * blockIdx.y;
+        e1 = e0 + chunk < e1 ? e0 + chunk : e1;
+    }
     // Each lane takes EB consecutive slots: slots are ordered by (column, row), so a lane's slots mostly
     // share a column and the column maximum is kept in a register, flushed to LDS when the column
     // changes (one LDS atomic per run instead of one per slot on a single, conflicting address).
@@ -472,7 +483,7 @@ __global__ __launch_bounds__(64) void k_sweep_front(SweepArgs A) {
         }
     };
     load(e0 + (int64_t)lane * EB);  // the first batch is in flight while the rows' scalings are gathered
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += NT) {
         rm[q] = 0ull;
         if (!FIRST) sl[q] = A.scale[A.rows[ro + q]];
     }
@@ -500,14 +511,18 @@ __global__ __launch_bounds__(64) void k_sweep_front(SweepArgs A) {
             }
         }
         if (cc >= 0) atomicMax(rm + cc, cm);
-        base += (int64_t)EB * 64;
+        base += (int64_t)EB * NT;
         if (base >= e1) break;  // uniform
         load(base + (int64_t)lane * EB);
     }
     __syncthreads();
-    for (int q = lane; q < m; q += 64) {
+    for (int q = lane; q < m; q += NT) {
         const int32_t r = A.rows[ro + q];
         const unsigned long long bw = rm[q];
+        if (BIG) {
+            if (bw != 0ull) atomicMax(A.rmax + r, bw);
+            continue;
+        }
         const int k = A.n_long > 0 ? (int)A.longpos[r] : -1;
         if (k >= 0) A.part_long[(int64_t)f * A.n_long + k] = as_double(bw);  // every front writes its slot
         else if (bw != 0ull) atomicMax(A.rmax + r, bw);
@@ -2688,8 +2703,10 @@ __global__ __launch_bounds__(64) void k_xpos(SolveArgs A, DfArgs D, int32_t* __r
 // ------------------------------------------------------------------------------------------------
 // The front lives in its FullStore (row-major, lower triangle used) and is factored in panels of at most
 // kBigNB pivots by a sequence of batched launches over the large fronts of one level:
-//   k_big_assemble  original entries + children's contribution blocks (assemble_front), row ids
-//   k_big_panel     one block per front: pivots of the next panel.  Column k is brought up to date
+//   k_big_init / k_big_entries / k_big_child   zero, original entries, children's contribution blocks
+//                   (the additions of assemble_front, same order), row ids -- 2-D grids (slices x fronts)
+//   k_big_panel_reg one block per front (m <= 4096): the next panel's pivots with the panel in registers
+//                   (below); k_big_panel for larger fronts: column k is brought up to date
 //                   left-looking (minus the panel's earlier pivots, L(i,q) W(k,q)), then tested with the
 //                   threshold rule; a pass is a 1x1 pivot.  On a failure with pivots pending the panel
 //                   ends (the trailing update must land first); on a failure at the panel's start every
@@ -2729,24 +2746,61 @@ __device__ __forceinline__ double block_max256(double v, double* red) {
     return r;
 }
 
-__global__ __launch_bounds__(kThreads) void k_big_assemble(FactorArgs A, const int32_t* __restrict__ fronts) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    const int f = fronts[blockIdx.x];
+// Assembly of the large fronts, spread over a 2-D grid (x: slices of the front, y: fronts) so an order-m
+// front is not assembled by one workgroup (m^2 stores plus the children's (m - p)^2 / 2 additions at one
+// CU's bandwidth was ~1 ms per front at m = 2048).  Three passes with the additions of assemble_front
+// in the same order per element: zero (+ row ids, state), original entries (distinct positions,
+// stored), then child 0, 1, ... (one launch each; a child's elements map to distinct parent positions).
+__global__ __launch_bounds__(kThreads) void k_big_init(FactorArgs A, const int32_t* __restrict__ fronts) {
+    const int f = fronts[blockIdx.y];
     const int m = A.fm[f], p = A.fp[f];
-    const FullStore st{A.gscratch + A.gscratch_off[f], m};
-    double* sloc = smem;
-    int32_t* lrow = (int32_t*)(sloc + m);
-    assemble_front<kThreads, false>(st, (int64_t)m * m, m, p, lrow, sloc, lrow, A, f);
-    const int64_t ro = A.rows_off[f];
-    for (int i = threadIdx.x; i < m; i += kThreads) {
-        A.frow[ro + i] = lrow[i];  // row ids, permuted in place by the interchanges
-        A.fpos[ro + i] = i;        // analysis-order local row of position i (inverted by k_big_finish)
+    double* F = A.gscratch + A.gscratch_off[f];
+    const int64_t tot = (int64_t)m * m;
+    for (int64_t t = (int64_t)blockIdx.x * kThreads + threadIdx.x; t < tot; t += (int64_t)gridDim.x * kThreads) F[t] = 0.0;
+    if (blockIdx.x == 0) {
+        const int64_t ro = A.rows_off[f];
+        for (int i = threadIdx.x; i < m; i += kThreads) {
+            A.frow[ro + i] = A.rows[ro + i];  // row ids, permuted in place by the interchanges
+            A.fpos[ro + i] = i;               // analysis-order local row of position i (inverted by k_big_finish)
+        }
+        if (threadIdx.x == 0) {
+            BigFrontState z{};
+            z.done = p == 0;
+            z.minpiv = INFINITY;
+            A.big[f] = z;
+        }
     }
-    if (threadIdx.x == 0) {
-        BigFrontState z{};
-        z.done = p == 0;
-        z.minpiv = INFINITY;
-        A.big[f] = z;
+}
+
+__global__ __launch_bounds__(kThreads) void k_big_entries(FactorArgs A, const int32_t* __restrict__ fronts) {
+    const int f = fronts[blockIdx.y];
+    const int m = A.fm[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const int64_t ro = A.rows_off[f];
+    const int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    for (int64_t e = e0 + (int64_t)blockIdx.x * kThreads + threadIdx.x; e < e1; e += (int64_t)gridDim.x * kThreads) {
+        const uint32_t lp = A.ent_lpos[e];
+        const int lr = (int)(lp >> 16), lc = (int)(lp & 0x7fffu);
+        const double sr = A.scale[A.rows[ro + lr]], sc = A.scale[A.rows[ro + lc]];
+        const double uv = A.uval[e];
+        st.at(lr, lc) = (lp & 0x8000u) ? sc * uv * sr : sr * uv * sc;  // assemble_front's multiplication order
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_big_child(FactorArgs A, const int32_t* __restrict__ fronts, int ci) {
+    const int f = fronts[blockIdx.y];
+    const int c = A.child_off[f] + ci;
+    if (c >= A.child_off[f + 1]) return;
+    const int m = A.fm[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const int cm = A.ch_cm[c];
+    const int32_t* rm = A.relmap + A.ch_relmap_off[c];
+    const double* cb = A.cb + A.ch_cb_off[c];
+    const int ctot = cm * (cm + 1) / 2;
+    for (int t = blockIdx.x * kThreads + threadIdx.x; t < ctot; t += gridDim.x * kThreads) {
+        int r, cc;
+        tri_rc(t, r, cc);
+        st.at(rm[r], rm[cc]) += cb[t];
     }
 }
 
@@ -2875,6 +2929,219 @@ __global__ __launch_bounds__(kThreads) void k_big_panel(FactorArgs A, const int3
     }
 }
 
+// Register-resident panel (fronts of m <= 256 * S; k_big_panel above stays for larger ones).  The
+// column-at-a-time left-looking loop of k_big_panel re-reads the panel's earlier columns from HBM for
+// every pivot (m * np scattered loads per step, ~40 us per pivot at m = 2048).  Here the panel rows
+// [k0, m) x columns [k0, k0 + NB) are loaded ONCE into registers -- thread t owns rows k0 + t + 256 s,
+// each row's NB columns one contiguous run of the row-major front -- and eliminated right-looking: per
+// pivot step the column's largest sub-diagonal magnitude (wave max tree + one workgroup barrier; the
+// diagonal block's column values through LDS, double-buffered by step parity so one barrier per step
+// suffices), the quick Duff-Reid 1x1 test of k_big_panel, then NB - c - 1 FMAs per owned row.  The
+// products are the left-looking ones of k_big_panel in the same order per element (L(i,q) = W(i,q) / d_q
+// times W(j,q), pivots q ascending), so the pivot sequence and counters follow the same rule.  A failure
+// at the panel's first column takes k_big_panel's exact search on the front in HBM (interchanges, 2x2,
+// null pivots, relaxation ladder, delays); its one or two pivots are applied to the reloaded register
+// panel (left-looking terms) and the panel continues.  A failure later ends the panel.  Only pivoted
+// columns are written back (un-normalised W, as k_big_panel stores them); the trailing columns stay
+// stale in HBM for k_big_update.
+template <int S, int NB, int T>
+__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 256))) void k_big_panel_reg(FactorArgs A, const int32_t* __restrict__ fronts) {
+    __shared__ double colk[2][NB], red[2][T / 64];
+    __shared__ double cA[4], cB[4];
+    __shared__ int bq[4];
+    __shared__ BigFrontState SF;
+    __shared__ FrontShared sh;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int f = fronts[blockIdx.x];
+    if (tid == 0) SF = A.big[f];
+    __syncthreads();
+    if (SF.done) {  // the last panel's update has been applied: nothing pending for k_big_update
+        if (tid == 0 && SF.k1 != SF.k0) { A.big[f].k0 = SF.k1; }
+        return;
+    }
+    const int m = A.fm[f], p = A.fp[f];
+    const int64_t ro = A.rows_off[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    int32_t* lrow = A.frow + ro;
+    int32_t* lorig = A.fpos + ro;
+    int8_t* piv = A.piv + ro;
+    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+    double minpiv = SF.minpiv;  // uniform
+    const int k0 = SF.k;
+    const int ncol = min(NB, p - k0);  // fully-summed columns of this panel
+    double P[S][NB];
+    auto load = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int r = k0 + tid + T * s;
+            const double* row = st.F + (int64_t)(r < m ? r : k0) * m + k0;
+#pragma unroll
+            for (int c = 0; c < NB; ++c) P[s][c] = (r < m && c < ncol) ? row[c] : 0.0;
+        }
+    };
+    // right-looking quick-test steps from register column cstart; returns the column where the panel stops
+    auto steps = [&](int cstart) __attribute__((always_inline)) -> int {
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+            if (c < cstart) continue;
+            if (c >= ncol) break;  // uniform
+            const int buf = c & 1;
+            double mx = 0.0;
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int r = k0 + tid + T * s;
+                mx = (r > k0 + c && r < m) ? fmax(mx, fabs(P[s][c])) : mx;
+            }
+            if (tid >= c && tid < NB) colk[buf][tid] = P[0][c];  // A(k0 + tid, k0 + c), diagonal block
+            mx = wave_max_abs(mx);
+            if (lane == 0) red[buf][wv] = mx;
+            __syncthreads();
+            double g = red[buf][0];
+#pragma unroll
+            for (int w = 1; w < T / 64; ++w) g = fmax(g, red[buf][w]);
+            const double akk = colk[buf][c];
+            const double aak = fabs(akk);
+            if (!(aak > thres) || A.u * g > aak) return c;  // uniform: the quick 1x1 test failed
+            const double dinv = 1.0 / akk;
+            minpiv = fmin(minpiv, aak);
+            double w[NB];
+#pragma unroll
+            for (int j = c + 1; j < NB; ++j) w[j] = colk[buf][j];
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const double l = P[s][c] * dinv;
+#pragma unroll
+                for (int j = c + 1; j < NB; ++j) P[s][j] -= l * w[j];
+            }
+            if (tid == 0) {  // pivot kinds are stored after the loop (a global store here would be waited for
+                             // by the next step's barrier)
+                if (akk > 0.0) SF.npos++; else SF.nneg++;
+            }
+        }
+        return ncol;
+    };
+    // quick 1x1 test of the panel's first column, current in HBM at the panel start; on a failure the
+    // exact search of the small-front kernels decides the first pivot(s) before the registers are loaded
+    int np = 0;  // pivots of the exact search (0, 1 or 2)
+    bool full = false;
+    if (ncol > 0) {
+        double g0 = 0.0;
+        for (int i = k0 + 1 + tid; i < m; i += T) g0 = fmax(g0, fabs(st.at(i, k0)));
+        g0 = wave_max_abs(g0);
+        if (lane == 0) red[0][wv] = g0;
+        __syncthreads();
+        g0 = red[0][0];
+#pragma unroll
+        for (int w = 1; w < T / 64; ++w) g0 = fmax(g0, red[0][w]);
+        __syncthreads();
+        const double a0 = fabs(st.at(k0, k0));
+        full = !(a0 > thres) || A.u * g0 > a0;
+    }
+    if (full) {
+        const int k = k0;
+        if (tid < 64) {
+            const PivotDecision d = search_pivot(st, m, k, p, A.u, thres, minpiv);
+            if (tid == 0) sh.dec = d;
+        }
+        __syncthreads();
+        PivotDecision d = sh.dec;
+        if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
+        if (d.c != k) {
+            sym_swap<T>(st, m, k, d.c, lrow, lorig);
+            __syncthreads();
+        }
+        if (d.kind == PIV_2X2_A) {
+            const int r = d.r == k ? d.c : d.r;
+            if (r != k + 1) {
+                sym_swap<T>(st, m, k + 1, r, lrow, lorig);
+                __syncthreads();
+            }
+        }
+        if (tid == 0) {
+            if (sh.dec.kind == PIV_STUCK) SF.nstuck++;
+            SF.nrel += d.relaxed;
+            if (d.relaxed && !SF.delays && A.record_delays && A.fparent[f] >= 0) {  // see factor_front
+                SF.delays = 1;
+                const unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
+                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
+            }
+        }
+        if (d.kind == PIV_NULL) {
+            for (int i = k + 1 + tid; i < m; i += T) st.at(i, k) = 0.0;
+            if (tid == 0) { piv[k] = PIV_NULL; SF.nzero++; cA[0] = 0.0; cB[0] = 0.0; bq[0] = k; }
+            np = 1;
+        } else if (d.kind == PIV_1X1) {
+            if (tid == 0) {
+                const double dk = st.at(k, k);
+                piv[k] = PIV_1X1;
+                if (dk > 0.0) SF.npos++; else SF.nneg++;
+                cA[0] = 1.0 / dk; cB[0] = 0.0; bq[0] = k;
+            }
+            np = 1;
+        } else {  // 2x2 on (k, k+1)
+            if (tid == 0) {
+                const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
+                const double det = a * e - b * b, idet = 1.0 / det;
+                piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; SF.n2++;
+                if (det < 0.0) { SF.npos++; SF.nneg++; }
+                else if (a + e > 0.0) SF.npos += 2;
+                else SF.nneg += 2;
+                cA[0] = e * idet; cB[0] = -b * idet; bq[0] = k;
+                cA[1] = -b * idet; cB[1] = a * idet; bq[1] = k;
+            }
+            np = 2;
+        }
+        __syncthreads();
+    }
+    load();
+    // the interchanged front minus the exact-search pivots' terms on the panel's later columns
+    for (int q = 0; q < np; ++q) {
+        const double ca = cA[q], cb = cB[q];
+        const int b0 = bq[q];
+        double lq[S];
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int r = k0 + tid + T * s;
+            double l = 0.0;
+            if (r < m) {
+                l = ca * st.at(r, b0);
+                if (cb != 0.0) l += cb * st.at(r, b0 + 1);
+            }
+            lq[s] = l;
+        }
+#pragma unroll
+        for (int j = 1; j < NB; ++j) {
+            if (j < np || j >= ncol) continue;
+            const double wj = st.at(k0 + j, k0 + q);  // W(j, q): row k0 + j > column k0 + q
+#pragma unroll
+            for (int s = 0; s < S; ++s) P[s][j] -= lq[s] * wj;
+        }
+    }
+    const int cw0 = np;  // first register column to write back
+    const int cend = steps(np);
+    // pivoted columns back to the front (lower part, un-normalised)
+#pragma unroll
+    for (int s = 0; s < S; ++s) {
+        const int r = k0 + tid + T * s;
+        if (r >= m) continue;
+        double* row = st.F + (int64_t)r * m + k0;
+#pragma unroll
+        for (int c = 0; c < NB; ++c)
+            if (c >= cw0 && c < cend && r >= k0 + c) row[c] = P[s][c];
+    }
+    for (int c = cw0 + tid; c < cend; c += T) piv[k0 + c] = PIV_1X1;
+    const int k = k0 + cend;
+    __syncthreads();  // counters of thread 0 complete
+    if (tid == 0) {
+        SF.minpiv = minpiv;
+        SF.k0 = k0;
+        SF.k1 = k;
+        SF.k = k;
+        SF.done = k >= p;
+        A.big[f] = SF;
+    }
+}
+
 // Trailing update of the pending panel [k0, k1): rows / columns [k1, m), lower triangle.  Block = one
 // 64 x 64 macro tile (blockIdx.x, lower-triangular order) of front fronts[blockIdx.y]; wave w owns rows
 // 16w .. 16w+15 of it and four 16 x 16 MFMA accumulators along the columns.
@@ -2954,19 +3221,23 @@ __global__ void k_big_pending(const FactorArgs A, const int32_t* __restrict__ fr
     if (threadIdx.x == 0) *out = red[0] + red[1] + red[2] + red[3];
 }
 
+// L, contribution block, row maps and counters of the large fronts: grid (x: slices, y: fronts); the
+// columns of L and the rows of the contribution block are spread over every wave of the slices, the row
+// map inversion and the counters are slice 0's.
 __global__ __launch_bounds__(kThreads) void k_big_finish(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     int32_t* lorig = (int32_t*)smem;
     const int tid = threadIdx.x;
-    const int f = fronts[blockIdx.x];
+    const int f = fronts[blockIdx.y];
     const int m = A.fm[f], p = A.fp[f];
     const int64_t ro = A.rows_off[f];
     const FullStore st{A.gscratch + A.gscratch_off[f], m};
     const int8_t* piv = A.piv + ro;
+    const int lane = tid & 63;
+    const int gw = blockIdx.x * (kThreads / 64) + (tid >> 6), nw = gridDim.x * (kThreads / 64);
     // L: packed lower trapezoid, column j rows j..m-1; one wave per column (coalesced stores)
     double* L = A.L + A.L_off[f];
-    const int lane = tid & 63;
-    for (int j = tid >> 6; j < p; j += kThreads / 64) {
+    for (int j = gw; j < p; j += nw) {
         double ca, cb;
         int base;
         piv_coefs(st, piv, j, ca, cb, base);
@@ -2983,17 +3254,18 @@ __global__ __launch_bounds__(kThreads) void k_big_finish(FactorArgs A, const int
             Lj[i] = v;
         }
     }
+    // contribution block: row-major packed lower triangle of order m - p
+    const int cm = m - p;
+    if (cm > 0) {
+        double* cbp = A.cb + A.cb_off[f];
+        for (int r = gw; r < cm; r += nw)
+            for (int c = lane; c <= r; c += 64) cbp[(int64_t)r * (r + 1) / 2 + c] = st.at(p + r, p + c);
+    }
+    if (blockIdx.x != 0) return;
     // analysis-order local row -> pivoted position
     for (int i = tid; i < m; i += kThreads) lorig[i] = A.fpos[ro + i];
     __syncthreads();
     for (int i = tid; i < m; i += kThreads) A.fpos[ro + lorig[i]] = i;
-    // contribution block: row-major packed lower triangle of order m - p
-    const int cm = m - p;
-    if (cm > 0) {
-        double* cb = A.cb + A.cb_off[f];
-        for (int r = tid >> 6; r < cm; r += kThreads / 64)
-            for (int c = lane; c <= r; c += 64) cb[(int64_t)r * (r + 1) / 2 + c] = st.at(p + r, p + c);
-    }
     if (tid == 0) {
         const BigFrontState S = A.big[f];
         A.fstat[f] = (int32_t)((S.nstuck > 0xffff ? 0xffff : S.nstuck) | ((S.nrel > 0x7fff ? 0x7fff : S.nrel) << 16));
@@ -3142,8 +3414,13 @@ hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s) {
     }
     for (int it = 0; it < (iters > 0 ? iters : 1); ++it) {
         if (A.nf > 0) {
-            if (it == 0) hipLaunchKernelGGL(k_sweep_front<true>, dim3((unsigned)A.nf), dim3(64), sh, s, A);
-            else hipLaunchKernelGGL(k_sweep_front<false>, dim3((unsigned)A.nf), dim3(64), sh, s, A);
+            if (it == 0) hipLaunchKernelGGL((k_sweep_front<true, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
+            else hipLaunchKernelGGL((k_sweep_front<false, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
+        }
+        if (A.n_big > 0) {
+            const dim3 gb((unsigned)A.n_big, (unsigned)A.big_slices);
+            if (it == 0) hipLaunchKernelGGL((k_sweep_front<true, true>), gb, dim3(256), sh, s, A);
+            else hipLaunchKernelGGL((k_sweep_front<false, true>), gb, dim3(256), sh, s, A);
         }
         if (A.n_long > 0) {
             const unsigned gl = (unsigned)std::min<int64_t>(256, (A.nf + 255) / 256);
@@ -3310,16 +3587,29 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
     return hipGetLastError();
 }
 
-hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
+// slices per large front: ~32 K elements of an order-mmax front per workgroup, at most 512
+static unsigned big_slices(int mmax) {
+    const int64_t el = (int64_t)mmax * mmax;
+    return (unsigned)std::max<int64_t>(1, std::min<int64_t>(512, el / 32768));
+}
+
+hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int count, int mmax, int maxch, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    const size_t sh = (size_t)mmax * (sizeof(double) + sizeof(int32_t)) + 16;
-    hipLaunchKernelGGL(k_big_assemble, dim3(count), dim3(kThreads), sh, s, A, fronts);
+    const dim3 g(big_slices(mmax), count);
+    hipLaunchKernelGGL(k_big_init, g, dim3(kThreads), 0, s, A, fronts);
+    hipLaunchKernelGGL(k_big_entries, g, dim3(kThreads), 0, s, A, fronts);
+    for (int c = 0; c < maxch; ++c) hipLaunchKernelGGL(k_big_child, g, dim3(kThreads), 0, s, A, fronts, c);
     return hipGetLastError();
 }
 
 hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_big_panel, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(double) + 16, s, A, fronts);
+    static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;  // diagnostics: the left-looking panel
+    if (legacy || mmax > 16 * kThreads) hipLaunchKernelGGL(k_big_panel, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(double) + 16, s, A, fronts);
+    else if (mmax <= 256) hipLaunchKernelGGL((k_big_panel_reg<1, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
+    else if (mmax <= 512) hipLaunchKernelGGL((k_big_panel_reg<2, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
+    else if (mmax <= 1024) hipLaunchKernelGGL((k_big_panel_reg<4, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
+    else hipLaunchKernelGGL((k_big_panel_reg<8, 8, 512>), dim3(count), dim3(512), 0, s, A, fronts);
     const int nt = (mmax + 63) / 64;
     hipLaunchKernelGGL(k_big_update, dim3(nt * (nt + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
     return hipGetLastError();
@@ -3332,11 +3622,14 @@ hipError_t launch_big_pending(const FactorArgs& A, const int32_t* fronts, int co
 
 hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_big_finish, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(int32_t) + 16, s, A, fronts);
+    hipLaunchKernelGGL(k_big_finish, dim3(big_slices(mmax), count), dim3(kThreads), (size_t)mmax * sizeof(int32_t) + 16, s, A, fronts);
     return hipGetLastError();
 }
 
-int big_panel_width() { return kBigNB; }
+int big_panel_width(int mmax) {
+    static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;
+    return (legacy || mmax > 16 * kThreads) ? kBigNB : (mmax > 1024 ? 8 : 16);
+}
 
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     if (A.df_nf <= 0) return hipSuccess;

@@ -162,6 +162,8 @@ struct SweepArgs {
     int32_t n_long;
     double* part_long;          // nf * n_long
     int max_m;
+    const int32_t* big_list;    // fronts of more than kSweepBigSlots slots (swept by 2-D grids)
+    int32_t n_big = 0, big_slices = 1;
 };
 hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s);
 hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
@@ -169,6 +171,7 @@ hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const
 // ||A_pre||_inf from the scaling by original id (row scans over the packed slots, no row-major copy)
 hipError_t launch_rowsum_norm_orig(ScanArgs A, double* rowsum, hipStream_t s);
 constexpr int kMaxSweepFront = 4096;  // largest front order of the front sweeps (LDS 16 B per row)
+constexpr int64_t kSweepBigSlots = 16384;  // fronts with more slots are swept by slices (k_sweep_front<., true>)
 
 // partial scans of the top (separator) rows on one rank: chunk c covers pslot[chunk_begin[c] ..
 // chunk_begin[c+1]) of top row chunk_row[c]; ppartner = original id of the slot's other index
@@ -223,11 +226,11 @@ hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, in
 
 // blocked large fronts (m > kMaxLdsFront): assemble, then (panel + MFMA trailing update) steps until
 // launch_big_pending reports no front still factoring, then finish (L, CB, row maps, counters)
-hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
+hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int count, int mmax, int maxch, hipStream_t s);
 hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
 hipError_t launch_big_pending(const FactorArgs& A, const int32_t* fronts, int count, int32_t* out, hipStream_t s);
 hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
-int big_panel_width();
+int big_panel_width(int mmax);  // pivots per panel step of the large-front launches
 
 // dataflow factorization of the upper tree (one-wave fronts, m <= 64)
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
