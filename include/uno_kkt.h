@@ -72,6 +72,8 @@ void uno_kkt_destroy(uno_kkt_t handle);
  * "max_block" (max supernode width, default 64), "wide_group" / "wide_block" (a separator or dense-row
  * group longer than wide_group = 128 columns is cut into supernodes of up to wide_block = 4096 columns,
  * factored as large fronts), "timing" (1 = per-kernel HIP event timing),
+ * "dist_dataflow_solve" (distributed runs: -1 = auto, on with the RCCL transport (one GPU per rank);
+ * 1 = each rank solves its own subtrees with the one-launch dataflow solve; 0 = level-scheduled),
  * "delay_relaxed" (default 1: a front whose fully-summed block has no pivot passing u is amalgamated
  * into its parent and refactored -- the delayed-pivot rule of MUMPS; 0 = accept relaxed pivots). */
 int uno_kkt_set_option(uno_kkt_t handle, const char* name, double value);

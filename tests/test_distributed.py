@@ -97,8 +97,10 @@ def rel_residual(ua, n, r, c, v, x, b):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("world", [2, 3, 4])
-def test_distributed_arrowband(ua, world):
+@pytest.mark.parametrize("world,dfs", [(2, 1), (3, 1), (4, 1), (2, 0), (3, 0)])
+def test_distributed_arrowband(ua, world, dfs):
+    """dfs = 1: each rank solves its own subtrees with the dataflow solve (one launch per direction), the
+    top of the tree level-scheduled on rank 0; dfs = 0: level-scheduled subtree solves."""
     n, nv, m, r, c, v, b = ua.arrowband(40000, ua.SEEDS["C2"])
     v2 = v.copy()
     v2[:nv] = 1e-2       # inertia-correction retry: primal regularization on the diagonal
@@ -109,9 +111,11 @@ def test_distributed_arrowband(ua, world):
     for vv in (v, v2):
         single.factorize(vv)
         ref.append((single.inertia(), single.solve(b)))
-    out = run_group(ua, world, n, r, c, (v, v2), b)
+    out = run_group(ua, world, n, r, c, (v, v2), b, dist_dataflow_solve=dfs)
     info0 = out[0][1]
     assert info0["world"] == world and info0["subtrees"] >= world
+    assert all((o[2]["solve_grid"] > 0) == bool(dfs) for o in out)
+    assert all(o[2]["solve_aborts"] == 0 for o in out)
     assert sum(o[1]["my_fronts"] for o in out) + info0["top_fronts"] == single.stats()["n_fronts"]
     # the ranks' own subtrees use the dataflow factorization of their upper levels too
     assert sum(o[2]["factor_df_fronts"] for o in out) > 0 and all(o[2]["factor_df_aborts"] == 0 for o in out)

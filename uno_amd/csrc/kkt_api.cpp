@@ -169,9 +169,20 @@ struct uno_kkt {
     unsigned long long* h_counters = nullptr;
     Plan plan[2];  // 0: the rank's own fronts (all fronts on one GPU), 1: top fronts (rank 0 of a group)
     Plan dff_plan; // factor launches of the own fronts outside the dataflow launch (dff active)
-    // dataflow solve (one launch per direction, kkt_kernels.hip k_solve_*_df); single GPU, every front
-    // one-wave eligible; option "dataflow_solve" (default 1)
+    // dataflow solve (one launch per direction, kkt_kernels.hip k_solve_*_df); every front of the walk
+    // one-wave eligible; option "dataflow_solve" (default 1).  The walk is every front on one GPU and the
+    // rank's own subtree fronts in distributed runs (option "dist_dataflow_solve"), whose top fronts stay
+    // level-scheduled on rank 0.  The walk assumes its grid is resident (sized by the occupancy query):
+    // default on with one GPU per rank (RCCL), off when ranks may share a GPU (in-process / host
+    // transports: waits would run into their bound and redo the solve level by level)
     int df_enabled = 1;
+    int dist_df = -1;              // -1: auto (RCCL transport)
+    bool own_device = false;       // the transport guarantees one GPU per rank
+    int32_t df_nwalk = 0;          // fronts of the walk
+    int64_t df_top_base = 0;       // distributed: xs slots of the top rows (top_orig order)
+    DBuf<int32_t> df_roots, df_topf;  // distributed: own subtree roots with a top parent; top fronts
+    int32_t n_df_roots = 0, n_df_topf = 0;
+    DBuf<unsigned long long> df_abort64;
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
     int df_win = 0, df_win_opt = 0; // LDS panel window of the dataflow solve (option solve_window, 0 = auto)
     int df_piv_off = 0;
@@ -323,7 +334,7 @@ int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, cons
 
 DfArgs dataflow_args(uno_kkt_t h) {
     DfArgs D;
-    D.order = h->df_order.p; D.desc = h->df_desc.p; D.nf = (int32_t)h->S.nf; D.parent = h->fparent.p; D.cnt = h->df_cnt.p;
+    D.order = h->df_order.p; D.desc = h->df_desc.p; D.nf = h->df_nwalk; D.parent = h->fparent.p; D.cnt = h->df_cnt.p;
     D.done = h->df_done.p; D.epoch = h->df_epoch; D.cvx = h->df_cvx.p; D.cvx_off = h->df_cvx_off.p;
     D.ch_cvx_off = h->df_ch_cvx_off.p; D.xs = h->df_xs.p; D.xs_off = h->df_xs_off.p; D.rxpos = h->df_rxpos.p;
     D.abort_flag = h->df_abort.p;
@@ -851,9 +862,17 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     h->df_grid = 0;
     h->df_rx_valid = false;
     h->df_epoch = 0;
-    if (h->world > 1 || !h->df_enabled || S.nf == 0) return hipSuccess;
+    h->df_nwalk = 0;
+    const bool dist = h->world > 1;
+    const bool dist_want = h->dist_df >= 0 ? h->dist_df != 0 : h->own_device;
+    if (!h->df_enabled || S.nf == 0 || (dist && !dist_want)) return hipSuccess;
+    std::vector<int32_t> walk;  // children before parents (level order)
+    walk.reserve(S.nf);
+    for (int32_t f : S.level_fronts)
+        if (!dist || h->dist.part.owner[f] == h->rank) walk.push_back(f);
+    if (walk.empty()) return hipSuccess;
     int max_sz = 0, mmax = 0;
-    for (int64_t f = 0; f < S.nf; ++f) {
+    for (int32_t f : walk) {
         const int m = S.f_m[f], p = S.f_p[f];
         if (p > 64 || m > kMaxLdsFront) {  // a front needs the 256-thread kernels
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve off: front %lld m %d p %d\n", (long long)f, m, p);
@@ -880,16 +899,30 @@ hipError_t setup_dataflow(uno_kkt_t h) {
         xs[f] = tx;
         tx += (S.f_p[f] + 15) & ~15;
     }
+    h->df_top_base = tx;
+    if (dist) tx += (h->dist.n_top_rows + 15) & ~15;
     if (tx >= INT32_MAX) return hipSuccess;
     for (size_t q = 0; q < S.child.size(); ++q) chx[q] = cvx[S.child[q]];
     hipStream_t s = h->stream;
     hipError_t e;
-    if ((e = h->df_order.upload(S.level_fronts, s)) != hipSuccess) return e;
+    if ((e = h->df_order.upload(walk, s)) != hipSuccess) return e;
+    if (dist) {
+        const Partition& Pt = h->dist.part;
+        std::vector<int32_t> roots, topf;
+        for (int32_t f = 0; f < (int32_t)S.nf; ++f) {
+            if (Pt.owner[f] < 0) topf.push_back(f);
+            else if (Pt.owner[f] == h->rank && S.f_parent[f] >= 0 && Pt.owner[S.f_parent[f]] < 0) roots.push_back(f);
+        }
+        h->n_df_roots = (int32_t)roots.size();
+        h->n_df_topf = (int32_t)topf.size();
+        if (!roots.empty() && (e = h->df_roots.upload(roots, s)) != hipSuccess) return e;
+        if (!topf.empty() && (e = h->df_topf.upload(topf, s)) != hipSuccess) return e;
+    }
     {
-        std::vector<int32_t> desc((size_t)S.nf * 16, 0);
+        std::vector<int32_t> desc(walk.size() * 16, 0);
         auto put64 = [&](int32_t* d, int64_t v) { d[0] = (int32_t)(uint32_t)v; d[1] = (int32_t)(uint32_t)((uint64_t)v >> 32); };
-        for (int64_t t = 0; t < S.nf; ++t) {
-            const int32_t f = S.level_fronts[t];
+        for (size_t t = 0; t < walk.size(); ++t) {
+            const int32_t f = walk[t];
             int32_t* d = desc.data() + 16 * t;
             d[kDescF] = f; d[kDescM] = S.f_m[f]; d[kDescP] = S.f_p[f]; d[kDescPar] = S.f_parent[f];
             d[kDescC0] = S.f_child_off[f]; d[kDescC1] = S.f_child_off[f + 1];
@@ -912,10 +945,11 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     if ((e = hipMemsetAsync(h->df_done.p, 0, sizeof(uint32_t) * S.nf, s)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s)) != hipSuccess) return e;
     h->df_lds = lds;
-    h->df_grid = solve_df_grid(lds, (int)S.nf);
+    h->df_nwalk = (int32_t)walk.size();
+    h->df_grid = solve_df_grid(lds, h->df_nwalk);
     if (h->verbose)
-        fprintf(stderr, "[uno_kkt] dataflow solve: %lld fronts, panel window %d of %d doubles, lds %d doubles, grid %d\n",
-                (long long)S.nf, win, max_sz, lds, h->df_grid);
+        fprintf(stderr, "[uno_kkt] dataflow solve: %d of %lld fronts, panel window %d of %d doubles, lds %d doubles, grid %d\n",
+                h->df_nwalk, (long long)S.nf, win, max_sz, lds, h->df_grid);
     return hipSuccess;
 }
 
@@ -1084,7 +1118,6 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, hipMemsetAsync(h->fstat.p, 0, sizeof(int32_t) * S.nf, s));
         HIPCHK(h, hipMemsetAsync(h->fcnt.p, 0, sizeof(unsigned long long) * S.nf, s));
     }
-    HIPCHK(h, setup_dataflow(h));
     if (h->world > 1) {
         int rc = setup_distribution(h);
         if (rc != UNO_KKT_OK) return rc;
@@ -1095,6 +1128,7 @@ int upload_structure(uno_kkt_t h) {
         HIPCHK(h, build_plan(h, [](int32_t) { return true; }, h->plan[0]));
         HIPCHK(h, build_plan(h, [](int32_t) { return false; }, h->plan[1]));
     }
+    HIPCHK(h, setup_dataflow(h));  // after the partition (distributed: the walk is the rank's own fronts)
     HIPCHK(h, setup_factor_dataflow(h));  // after the partition: a rank's own subtrees
     HIPCHK(h, hipStreamSynchronize(s));
     double an = h->st.analysis_seconds;
@@ -1372,6 +1406,13 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }
+    else if (n == "dist_dataflow_solve") {
+        h->dist_df = value < 0.0 ? -1 : value != 0.0;
+        if (h->analyzed) {
+            HIPCHK(h, setup_dataflow(h));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+    }
     else if (n == "dataflow_solve") {
         h->df_enabled = value != 0.0;
         if (h->analyzed) {
@@ -1529,7 +1570,8 @@ namespace {
 int solve_core(uno_kkt_t h, const double* b, double* xd) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
-    const bool df = h->world == 1 && h->df_enabled && h->df_grid > 0;
+    const bool df = h->df_enabled && h->df_grid > 0;
+    const bool dist = h->world > 1;
     SolveArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
@@ -1542,41 +1584,45 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
     };
     const Plan& P0 = h->plan[0];
     const Plan& P1 = h->plan[1];
-    if (!df) {
+    if (!df || dist) {  // level schedule (distributed: rank 0's top fronts read the scaled rhs from w)
         TimerScope t(h, KC_RHS);
         HIPCHK(h, launch_rhs_scale(b, h->scale.p, h->w.p, S.n, s));
     }
+    DfArgs Df;
     if (df) {
-        DfArgs D = dataflow_args(h);
+        Df = dataflow_args(h);
         if (!h->df_rx_valid) {
-            HIPCHK(h, launch_xpos(A, D, h->df_xpos.p, h->df_rxpos.p, s));
+            HIPCHK(h, launch_xpos(A, Df, h->df_xpos.p, h->df_rxpos.p, dist ? h->dist.top_orig.p : nullptr,
+                                  dist ? h->dist.n_top_rows : 0, h->df_top_base, s));
             h->df_rx_valid = true;
         }
         {
             TimerScope t(h, KC_RHS);
-            HIPCHK(h, launch_xs_in(b, h->scale.p, h->df_xpos.p, h->df_xs.p, S.n, s));
+            HIPCHK(h, launch_xs_in(b, h->scale.p, h->df_xpos.p, h->df_xs.p, dist ? h->dist.n_own : S.n, s,
+                                   dist ? h->dist.own_orig.p : nullptr));
         }
-        D.epoch = ++h->df_epoch;
+        Df.epoch = ++h->df_epoch;
         if (h->want_solve_stamps) {
             if (h->df_stamps.n != (size_t)(8 * S.nf)) HIPCHK(h, h->df_stamps.alloc(8 * S.nf));
-            D.stamps = h->df_stamps.p;
+            Df.stamps = h->df_stamps.p;
         }
         {
             TimerScope t(h, KC_SOLVE_FWD);
-            HIPCHK(h, launch_solve_df(A, D, h->df_grid, h->df_lds, true, s));
+            HIPCHK(h, launch_solve_df(A, Df, h->df_grid, h->df_lds, true, s));
         }
-        {
+        if (!dist) {
             TimerScope t(h, KC_SOLVE_BWD);
-            HIPCHK(h, launch_solve_df(A, D, h->df_grid, h->df_lds, false, s));
+            HIPCHK(h, launch_solve_df(A, Df, h->df_grid, h->df_lds, false, s));
         }
     }
     for (size_t q = 0; q < P0.sol.size() && !df; ++q) {
         TimerScope t(h, KC_SOLVE_FWD);
         HIPCHK(h, run(P0, P0.sol[q], true));
     }
-    if (h->world > 1) {
+    if (dist) {
         DistState& D = h->dist;
         // forward: subtree roots' update vectors -> rank 0, which solves the top of the tree
+        if (df) HIPCHK(h, launch_cvx_to_cvec(Df, A, h->df_roots.p, h->n_df_roots, h->cvec.p, s));
         int rc = exchange_roots(h, h->cvec.p, [&](int32_t f) { return S.f_relmap_off[f]; },
                                 [&](int32_t f) { return (int64_t)(S.f_m[f] - S.f_p[f]); });
         if (rc != UNO_KKT_OK) return rc;
@@ -1592,7 +1638,17 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
         if (D.n_top_rows > 0) {
             if (h->rank == 0) HIPCHK(h, launch_gather(h->w.p, D.top_orig.p, D.tbuf.p, D.n_top_rows, s));
             HIPCHK(h, h->comm->broadcast(D.tbuf.p, sizeof(double) * D.n_top_rows, 0, s));
-            if (h->rank != 0) HIPCHK(h, launch_scatter(D.tbuf.p, D.top_orig.p, h->w.p, D.n_top_rows, s));
+            if (df) {
+                HIPCHK(h, hipMemcpyAsync(h->df_xs.p + h->df_top_base, D.tbuf.p, sizeof(double) * D.n_top_rows,
+                                         hipMemcpyDeviceToDevice, s));
+            } else if (h->rank != 0) {
+                HIPCHK(h, launch_scatter(D.tbuf.p, D.top_orig.p, h->w.p, D.n_top_rows, s));
+            }
+        }
+        if (df) {  // the subtree roots' parents (top fronts) have published
+            HIPCHK(h, launch_set_done(h->df_done.p, h->df_topf.p, h->n_df_topf, Df.epoch, s));
+            TimerScope t(h, KC_SOLVE_BWD);
+            HIPCHK(h, launch_solve_df(A, Df, h->df_grid, h->df_lds, false, s));
         }
     }
     for (size_t q = P0.sol.size(); q-- > 0 && !df;) {
@@ -1601,10 +1657,16 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
     }
     {
         TimerScope t(h, KC_RHS);
-        if (df) HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, S.n, s));
-        else HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
+        if (df && dist) {  // own rows and top rows (the rows a rank's solution holds)
+            HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, h->dist.n_own, s, h->dist.own_orig.p));
+            HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, h->dist.n_top_rows, s, h->dist.top_orig.p));
+        } else if (df) {
+            HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, S.n, s));
+        } else {
+            HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
+        }
     }
-    if (h->world > 1 && h->gather_solution) {
+    if (dist && h->gather_solution) {
         // MUMPS-style centralized solution on rank 0 (ICNTL(21) = 0): own rows of every other rank
         DistState& D = h->dist;
         if (h->rank != 0 && D.n_own > 0) HIPCHK(h, launch_gather(xd, D.own_orig.p, D.xbuf.p, D.n_own, s));
@@ -1619,13 +1681,24 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
         if (h->rank == 0)
             HIPCHK(h, launch_scatter(D.xbuf.p, D.all_own_orig.p, xd, D.all_own_off[h->world], s));
     }
-    if (df) {
+    if (df || dist) {
         // a dataflow solve is checked in the same call: on an abort k_xs_out has left x (and so an aliased
-        // rhs) untouched, and the solve is redone with the level schedule
-        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        // rhs) untouched, and the solve is redone with the level schedule.  Distributed: every rank takes
+        // part in the all-reduce of the abort flag (a rank whose walk is empty or ineligible runs the
+        // level schedule and contributes 0), and every rank redoes the solve if any aborted, so the ranks
+        // keep taking the same path through the collectives
+        if (dist) {
+            if (!h->df_abort64.p) HIPCHK(h, h->df_abort64.alloc(1));
+            HIPCHK(h, hipMemsetAsync(h->df_abort64.p, 0, sizeof(unsigned long long), s));
+            if (df) HIPCHK(h, hipMemcpyAsync(h->df_abort64.p, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+            HIPCHK(h, h->comm->allreduce(h->df_abort64.p, 1, RedOp::MaxU64, s));
+            HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort64.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        } else {
+            HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        }
         HIPCHK(h, hipStreamSynchronize(s));
         if (dataflow_aborted(h)) {
-            HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
+            if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: redone level by level\n");
             return solve_core(h, b, xd);
         }
@@ -1685,7 +1758,7 @@ int uno_kkt_stats(uno_kkt_t h, uno_kkt_stats_t* out) {
     }
     *out = h->st;
     out->fronts_merged = h->merges_total;
-    out->solve_grid = (h->world == 1 && h->df_enabled) ? h->df_grid : 0;
+    out->solve_grid = h->df_enabled ? h->df_grid : 0;
     out->solve_aborts = h->df_aborts;
     out->factor_df_fronts = h->dff_level != INT32_MAX ? (int64_t)h->dff_order.n : 0;
     out->factor_df_aborts = h->dff_aborts;
@@ -1952,6 +2025,7 @@ int uno_kkt_comm_unique_id(unsigned char id[128]) {
 static int attach(uno_kkt_t h, ukkt::Transport* t) {
     delete h->comm;
     h->comm = t;
+    h->own_device = false;
     h->rank = t->rank();
     h->world = t->size();
     h->analyzed = h->factored = h->factor_enqueued = false;
@@ -1963,7 +2037,9 @@ int uno_kkt_attach_rccl(uno_kkt_t h, const unsigned char id[128], int rank, int 
     std::string err;
     ukkt::Transport* t = ukkt::make_rccl_transport(id, rank, world, h->device, err);
     if (!t) return set_err(h, UNO_KKT_ERR_HIP, err);
-    return attach(h, t);
+    const int rc = attach(h, t);
+    h->own_device = true;  // RCCL refuses two ranks on one GPU
+    return rc;
 }
 
 int uno_kkt_group_create(uno_kkt_group_t* g, int world) {

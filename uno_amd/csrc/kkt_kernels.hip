@@ -2672,22 +2672,45 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 
 // right-hand side into elimination order (xs[xpos[i]] = s_i b_i) and the solution back (x_i = s_i xs[xpos[i]])
 __global__ void k_xs_in(const double* __restrict__ b, const double* __restrict__ scale, const int32_t* __restrict__ xpos,
-                        double* __restrict__ xs, int64_t n) {
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+                        double* __restrict__ xs, int64_t n, const int32_t* __restrict__ list) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = list ? list[t] : t;
         xs[xpos[i]] = scale[i] * b[i];
+    }
 }
 __global__ void k_xs_out(const double* __restrict__ xs, const double* __restrict__ scale, const int32_t* __restrict__ xpos,
-                         const uint32_t* __restrict__ abort_flag, double* __restrict__ x, int64_t n) {
+                         const uint32_t* __restrict__ abort_flag, double* __restrict__ x, int64_t n, const int32_t* __restrict__ list) {
     if (*abort_flag) return;  // aborted dataflow solve: x (possibly aliasing the rhs) is left untouched
-    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = list ? list[t] : t;
         x[i] = scale[i] * xs[xpos[i]];
+    }
+}
+__global__ void k_xpos_top(const int32_t* __restrict__ top_orig, int64_t n_top, int64_t top_base, int32_t* __restrict__ xpos) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n_top; t += (int64_t)gridDim.x * blockDim.x)
+        xpos[top_orig[t]] = (int32_t)(top_base + t);
+}
+__global__ __launch_bounds__(64) void k_cvx_to_cvec(DfArgs D, SolveArgs A, const int32_t* __restrict__ roots, int count,
+                                                    double* __restrict__ cvec) {
+    for (int r = blockIdx.x; r < count; r += gridDim.x) {
+        const int f = roots[r];
+        const int cm = A.fm[f] - A.fp[f];
+        const double* src = D.cvx + D.cvx_off[f];
+        double* dst = cvec + A.relmap_off[f];
+        for (int t = threadIdx.x; t < cm; t += 64) dst[t] = src[t];
+    }
+}
+__global__ void k_set_done(uint32_t* __restrict__ done, const int32_t* __restrict__ list, int count, uint32_t epoch) {
+    for (int t = blockIdx.x * blockDim.x + threadIdx.x; t < count; t += gridDim.x * blockDim.x)
+        __hip_atomic_store(done + list[t], epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // Per-factorization map for the dataflow backward solve: rxpos[row slot] = xs index of the row's
 // solution value (pass 0: xpos[original id] of every pivot; pass 1: rows >= p of every front).
 __global__ __launch_bounds__(64) void k_xpos(SolveArgs A, DfArgs D, int32_t* __restrict__ xpos, int32_t* __restrict__ rxpos,
                                              int pass) {
-    for (int f = blockIdx.x; f < D.nf; f += gridDim.x) {
+    for (int t = blockIdx.x; t < D.nf; t += gridDim.x) {  // the walk's fronts
+        const int f = D.order[t];
         const int m = A.fm[f], p = A.fp[f];
         const int64_t ro = A.rows_off[f];
         if (pass == 0) {
@@ -3664,24 +3687,39 @@ hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int ld
     return hipGetLastError();
 }
 
-hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s) {
+hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s,
+                        const int32_t* list) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_xs_in, dim3(grid_for(n, 256)), dim3(256), 0, s, b, scale, xpos, xs, n);
+    hipLaunchKernelGGL(k_xs_in, dim3(grid_for(n, 256)), dim3(256), 0, s, b, scale, xpos, xs, n, list);
     return hipGetLastError();
 }
 
 hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, const uint32_t* abort_flag, double* x,
-                         int64_t n, hipStream_t s) {
+                         int64_t n, hipStream_t s, const int32_t* list) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, abort_flag, x, n);
+    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, abort_flag, x, n, list);
     return hipGetLastError();
 }
 
-hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, hipStream_t s) {
+hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
+                       int64_t n_top, int64_t top_base, hipStream_t s) {
     if (D.nf <= 0) return hipSuccess;
     const int g = std::min(D.nf, 8192);
     hipLaunchKernelGGL(k_xpos, dim3(g), dim3(64), 0, s, A, D, xpos, rxpos, 0);
+    if (n_top > 0) hipLaunchKernelGGL(k_xpos_top, dim3(grid_for(n_top, 256)), dim3(256), 0, s, top_orig, n_top, top_base, xpos);
     hipLaunchKernelGGL(k_xpos, dim3(g), dim3(64), 0, s, A, D, xpos, rxpos, 1);
+    return hipGetLastError();
+}
+
+hipError_t launch_cvx_to_cvec(const DfArgs& D, const SolveArgs& A, const int32_t* roots, int count, double* cvec, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_cvx_to_cvec, dim3(std::min(count, 4096)), dim3(64), 0, s, D, A, roots, count, cvec);
+    return hipGetLastError();
+}
+
+hipError_t launch_set_done(uint32_t* done, const int32_t* list, int count, uint32_t epoch, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_set_done, dim3(grid_for(count, 256)), dim3(256), 0, s, done, list, count, epoch);
     return hipGetLastError();
 }
 

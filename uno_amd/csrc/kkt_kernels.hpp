@@ -238,12 +238,20 @@ hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
 int solve_df_grid(int lds_doubles, int nf);
 int solve_slack_doubles();
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
-// rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch
-hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, hipStream_t s);
-// xs[xpos[i]] = scale_i b_i  /  x_i = scale_i xs[xpos[i]]
-hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s);
+// rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch.  Distributed
+// runs: the walk is the rank's own fronts, and the top rows (top_orig, eliminated on rank 0) get the
+// slots top_base + t of xs, where the broadcast top solution is copied before the backward launch
+hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
+                       int64_t n_top, int64_t top_base, hipStream_t s);
+// xs[xpos[i]] = scale_i b_i  /  x_i = scale_i xs[xpos[i]]; rows i = list[0 .. n) (list == nullptr: 0 .. n-1)
+hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s,
+                        const int32_t* list = nullptr);
 hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, const uint32_t* abort_flag, double* x,
-                         int64_t n, hipStream_t s);
+                         int64_t n, hipStream_t s, const int32_t* list = nullptr);
+// distributed dataflow solve: subtree roots' update vectors (cvx slots) -> cvec (level-schedule layout,
+// sent to rank 0); done[f] = epoch for the top fronts (the subtree roots' parents) before the backward
+hipError_t launch_cvx_to_cvec(const DfArgs& D, const SolveArgs& A, const int32_t* roots, int count, double* cvec, hipStream_t s);
+hipError_t launch_set_done(uint32_t* done, const int32_t* list, int count, uint32_t epoch, hipStream_t s);
 
 constexpr int kMaxLdsFront = 128;
 constexpr int kMaxWaveFront = 72;     // one-wave register-resident factorization (8 x 8 lane grid, 9 row blocks)     // fronts up to this order factor entirely in LDS
