@@ -137,6 +137,7 @@ __global__ void k_symv(SymvArgs A) {
     const int lane = threadIdx.x & 15;
     if (g >= A.n) return;
     const int32_t i = (int32_t)g;
+    if ((int64_t)(A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > A.long_len) return;  // k_symv_long
     const int32_t oi = A.perm[i];
     double acc = 0.0;
     for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += 16) acc += A.uval[q] * A.x[A.ent_r[q]];
@@ -149,6 +150,46 @@ __global__ void k_symv(SymvArgs A) {
         A.y[oi] += acc;
         if (A.dot_w) A.dot_part[i] = A.dot_w[oi] * acc;
     }
+}
+
+// long rows: block (chunk c, long row k) sums the row's entries [c, c + 1) * kSymvChunk (column part,
+// then row part, as k_symv walks them) in a fixed tree order into long_part[k * long_chunks + c]
+__global__ void k_symv_long(SymvArgs A) {
+    __shared__ double red[kT / 64];
+    const int k = blockIdx.y;
+    const int32_t i = A.long_rows[k];
+    const int32_t c0 = A.cptr[i], nc = A.cptr[i + 1] - c0;
+    const int32_t r0 = A.rptr[i], len = nc + (A.rptr[i + 1] - r0);
+    const int32_t b = blockIdx.x * kSymvChunk, e = min(len, b + kSymvChunk);
+    double acc = 0.0;
+    for (int32_t t = b + threadIdx.x; t < e; t += kT) {
+        if (t < nc) {
+            const int32_t q = c0 + t;
+            acc += A.uval[q] * A.x[A.ent_r[q]];
+        } else {
+            const int32_t q = A.rslot[r0 + (t - nc)];
+            acc += A.uval[q] * A.x[A.ent_c[q]];
+        }
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = red[0];
+        for (int w = 1; w < kT / 64; ++w) s += red[w];
+        A.long_part[(int64_t)k * A.long_chunks + blockIdx.x] = s;  // 0 for chunks past the row's end
+    }
+}
+
+__global__ void k_symv_long_fin(SymvArgs A) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.n_long) return;
+    const int32_t i = A.long_rows[k];
+    const int32_t oi = A.perm[i];
+    double acc = 0.0;
+    for (int c = 0; c < A.long_chunks; ++c) acc += A.long_part[(int64_t)k * A.long_chunks + c];
+    A.y[oi] += acc;
+    if (A.dot_w) A.dot_part[i] = A.dot_w[oi] * acc;
 }
 
 // sum of per-row partials (quadratic_product): one block-sum per workgroup, atomics on one double
@@ -214,6 +255,10 @@ hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     const int64_t threads = A.n * 16;
     hipLaunchKernelGGL(k_symv, dim3((unsigned)((threads + kT - 1) / kT)), dim3(kT), 0, s, A);
+    if (A.n_long > 0) {
+        hipLaunchKernelGGL(k_symv_long, dim3((unsigned)A.long_chunks, (unsigned)A.n_long), dim3(kT), 0, s, A);
+        hipLaunchKernelGGL(k_symv_long_fin, dim3((unsigned)((A.n_long + 63) / 64)), dim3(64), 0, s, A);
+    }
     if (A.dot_w) {
         hipError_t e = hipMemsetAsync(dot_out, 0, sizeof(double), s);
         if (e != hipSuccess) return e;

@@ -36,7 +36,14 @@ struct SymvArgs {
     double* y;            // y += A x, by original index
     const double* dot_w;  // optional: w^T A x partials (quadratic_product), by original index
     double* dot_part;     // per row (new numbering)
+    // rows with more than long_len entries (the dense "arrow" rows: 2.5e5 entries each at C3), reduced by
+    // chunks of kSymvChunk over a 2-D grid instead of 16 lanes (14 ms -> microseconds)
+    int64_t long_len = INT64_MAX;
+    const int32_t* long_rows = nullptr;  // new numbering
+    int32_t n_long = 0, long_chunks = 0;
+    double* long_part = nullptr;         // n_long * long_chunks chunk partials (summed in chunk order)
 };
+constexpr int kSymvChunk = 4096;
 
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
                       const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s);

@@ -158,6 +158,7 @@ struct uno_kkt {
     int front_sweeps = 1;                 // option front_sweeps: equilibration over the fronts' slots (k_sweep_front)
     bool use_front_sweeps = false;        // front_sweeps, one GPU and every front within kMaxSweepFront rows
     DBuf<int8_t> longpos;                 // by original id: index among the long rows, -1 otherwise
+    DBuf<double> symv_long_part;          // symv: chunk partials of the long rows
     DBuf<int32_t> sweep_big;              // fronts of more than kSweepBigSlots slots (sliced sweeps)
     int32_t n_sweep_big = 0, sweep_slices = 1;
     DBuf<int32_t> long_orig;              // long rows, original ids
@@ -1982,6 +1983,13 @@ int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* 
     A.n = S.n; A.perm = h->perm_d.p; A.cptr = h->cptr.p; A.rptr = h->rptr.p; A.rslot = h->rslot.p;
     A.ent_r = h->ent_r.p; A.ent_c = h->ent_c.p; A.uval = h->uval.p; A.x = x; A.y = y; A.dot_w = w;
     A.dot_part = nullptr;
+    if (h->n_long > 0) {
+        const int32_t nch = (int32_t)((h->max_long + kSymvChunk - 1) / kSymvChunk);
+        const size_t need = (size_t)h->n_long * nch;
+        if (h->symv_long_part.n < need) HIPCHK(h, h->symv_long_part.alloc(need));
+        A.long_len = kLongRow; A.long_rows = h->long_rows.p; A.n_long = h->n_long; A.long_chunks = nch;
+        A.long_part = h->symv_long_part.p;
+    }
     if (w) {
         if (h->symv_part.n != (size_t)S.n) HIPCHK(h, h->symv_part.alloc(std::max<int64_t>(S.n, 1)));
         if (!h->dot_d.p) HIPCHK(h, h->dot_d.alloc(1));
