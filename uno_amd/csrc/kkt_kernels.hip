@@ -16,6 +16,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
+#include <type_traits>
 
 #include "kkt_kernels.hpp"
 
@@ -2967,11 +2968,13 @@ __global__ __launch_bounds__(kThreads) void k_big_panel(FactorArgs A, const int3
 // panel (left-looking terms) and the panel continues.  A failure later ends the panel.  Only pivoted
 // columns are written back (un-normalised W, as k_big_panel stores them); the trailing columns stay
 // stale in HBM for k_big_update.
-template <int S, int NB, int T>
+template <int S, int NB, int T, bool SEARCH = true>
 __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 256))) void k_big_panel_reg(FactorArgs A, const int32_t* __restrict__ fronts) {
     __shared__ double colk[2][NB], red[2][T / 64];
     __shared__ double cA[4], cB[4];
     __shared__ int bq[4];
+    __shared__ double rowK[NB], rowC[NB], colX[NB], sred[T / 64];  // in-panel search / interchange
+    __shared__ unsigned long long ured[T / 64];
     __shared__ BigFrontState SF;
     __shared__ FrontShared sh;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2992,14 +2995,18 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
     double minpiv = SF.minpiv;  // uniform
     const int k0 = SF.k;
     const int ncol = min(NB, p - k0);  // fully-summed columns of this panel
-    double P[S][NB];
+    // one vector register tuple per owned row: static columns in the pivot steps, dynamic (uniform) ones in
+    // the in-panel search via indexed register moves -- never scratch
+    typedef double RowV __attribute__((ext_vector_type(NB)));
+    typedef double RowA[NB];
+    typename std::conditional<SEARCH, RowV, RowA>::type P[S];
     auto load = [&]() __attribute__((always_inline)) {
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int r = k0 + tid + T * s;
             const double* row = st.F + (int64_t)(r < m ? r : k0) * m + k0;
 #pragma unroll
-            for (int c = 0; c < NB; ++c) P[s][c] = (r < m && c < ncol) ? row[c] : 0.0;
+            for (int c = 0; c < NB; ++c) P[s][c] = (r < m && k0 + c < m) ? row[c] : 0.0;
         }
     };
     // right-looking quick-test steps from register column cstart; returns the column where the panel stops
@@ -3134,15 +3141,152 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         }
 #pragma unroll
         for (int j = 1; j < NB; ++j) {
-            if (j < np || j >= ncol) continue;
+            if (j < np || k0 + j >= m) continue;
             const double wj = st.at(k0 + j, k0 + q);  // W(j, q): row k0 + j > column k0 + q
 #pragma unroll
             for (int s = 0; s < S; ++s) P[s][j] -= lq[s] * wj;
         }
     }
     const int cw0 = np;  // first register column to write back
-    const int cend = steps(np);
-    // pivoted columns back to the front (lower part, un-normalised)
+    // ---- exact search restricted to the panel ----
+    // At a column c whose quick test fails, the exact rule (search_pivot, first threshold level) examines
+    // the candidates c, c+1, ... in order.  The panel's columns are current for every row, so as long as
+    // the candidates lie in the panel the same tests are evaluated here; a 1x1 acceptance is applied by a
+    // symmetric interchange in the registers (+ the rows' earlier columns in HBM) and the panel goes on.
+    // Anything else -- a null pivot, a 2x2 the rule would take, a 2x2 partner outside the panel, no
+    // candidate left in the panel -- ends the call; the exact search then runs on the updated front.
+    auto pget = [&](int s, int j) __attribute__((always_inline)) -> double { return P[s][j]; };
+    auto bmax = [&](double v) __attribute__((always_inline)) -> double {  // non-negative values
+        v = wave_max_abs(v);
+        if (lane == 0) sred[wv] = v;
+        __syncthreads();
+        double r = sred[0];
+#pragma unroll
+        for (int w = 1; w < T / 64; ++w) r = fmax(r, sred[w]);
+        __syncthreads();
+        return r;
+    };
+    auto bmaxu = [&](unsigned long long v) __attribute__((always_inline)) -> unsigned long long {
+        v = wave_max_u64(v);
+        if (lane == 0) ured[wv] = v;
+        __syncthreads();
+        unsigned long long r = ured[0];
+#pragma unroll
+        for (int w = 1; w < T / 64; ++w) r = umax64(r, ured[w]);
+        __syncthreads();
+        return r;
+    };
+    // max |A(i, col j)| over rows i >= k0 + c, i not in {k0 + j, k0 + x}: rows below from the column,
+    // rows in [k0 + c, k0 + j) from row k0 + j (upper triangle by symmetry)
+    auto colmax = [&](int c, int j, int x) __attribute__((always_inline)) -> double {
+        double g = 0.0;
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int r = k0 + tid + T * s;
+            const double v = fabs(pget(s, j));
+            if (r > k0 + j && r < m && r != k0 + x) g = fmax(g, v);
+        }
+        if (tid == j)
+            for (int i = c; i < j; ++i)
+                if (i != x) g = fmax(g, fabs(pget(0, i)));
+        return bmax(g);
+    };
+    auto search = [&](int c) __attribute__((always_inline)) -> bool {
+        const int k = k0 + c;
+        for (int j = c; j < ncol; ++j) {
+            const int cand = k0 + j;
+            if (tid == j) colX[0] = pget(0, j);  // A(cand, cand)
+            const double g = colmax(c, j, -1);   // (barriers inside)
+            const double ajj = colX[0], acc = fabs(ajj);
+            if (fmax(acc, g) <= thres) return false;  // null pivot: the exact search decides
+            minpiv = fmin(minpiv, fmax(acc, g));
+            if (acc != 0.0 && acc >= A.u * g) {
+                if (j == c) return true;
+                // symmetric interchange of rows / columns k and cand (sym_swap in the register layout)
+                if (tid == c) for (int q = 0; q < NB; ++q) rowK[q] = pget(0, q);
+                if (tid == j) for (int q = 0; q < NB; ++q) rowC[q] = pget(0, q);
+                if (tid > c && tid < j) colX[tid] = pget(0, c);
+                __syncthreads();
+#pragma unroll
+                for (int s = 0; s < S; ++s) {
+                    const int r = k0 + tid + T * s;
+                    if (r > cand && r < m) {  // rows below both: the two columns trade places
+                        const double vc = pget(s, c), vj = pget(s, j);
+#pragma unroll
+                        for (int jj = 0; jj < NB; ++jj) P[s][jj] = jj == c ? vj : (jj == j ? vc : P[s][jj]);
+                    }
+                }
+                if (tid == c) {  // row k <- row cand: columns < c, and the diagonal
+#pragma unroll
+                    for (int jj = 0; jj < NB; ++jj) P[0][jj] = jj < c ? rowC[jj] : (jj == c ? rowC[j] : P[0][jj]);
+                } else if (tid == j) {  // row cand <- row k: columns < c, (k, cand) rows' column k, diagonal
+#pragma unroll
+                    for (int jj = 0; jj < NB; ++jj)
+                        P[0][jj] = jj < c ? rowK[jj] : (jj > c && jj < j ? colX[jj] : (jj == j ? rowK[c] : P[0][jj]));
+                } else if (tid > c && tid < j) {  // A(i, k) <- A(cand, i)
+#pragma unroll
+                    for (int jj = 0; jj < NB; ++jj) P[0][jj] = jj == c ? rowC[tid] : P[0][jj];
+                }
+                // the two rows in the columns before the registers' write-back range, row ids
+                for (int q = tid; q < k0 + cw0; q += T) {
+                    const double a = st.F[(int64_t)k * m + q], b = st.F[(int64_t)cand * m + q];
+                    st.F[(int64_t)k * m + q] = b;
+                    st.F[(int64_t)cand * m + q] = a;
+                }
+                if (tid == 0) {
+                    int32_t y = lrow[k]; lrow[k] = lrow[cand]; lrow[cand] = y;
+                    y = lorig[k]; lorig[k] = lorig[cand]; lorig[cand] = y;
+                }
+                __syncthreads();
+                return true;
+            }
+            // 1x1 rejected: the largest off-diagonal among the fully-summed rows is the 2x2 partner
+            unsigned long long best = 0;
+            int bi = 0x7fffffff;
+            if (tid == j)
+                for (int i = c; i < j; ++i) {
+                    const unsigned long long b = as_bits(fabs(pget(0, i)));
+                    if (b > best) { best = b; bi = k0 + i; }
+                }
+#pragma unroll
+            for (int s = 0; s < S; ++s) {
+                const int r = k0 + tid + T * s;
+                if (r > cand && r < p && r < m) {
+                    const unsigned long long b = as_bits(fabs(pget(s, j)));
+                    if (b > best) { best = b; bi = r; }
+                }
+            }
+            const unsigned long long mx = bmaxu(best);
+            if (mx == 0) continue;
+            const unsigned long long ik = bmaxu(best == mx ? 0xffffffffull - (unsigned)bi : 0ull);
+            const int r = (int)(0xffffffffull - ik);
+            const int jr = r - k0;
+            if (jr >= ncol) return false;  // partner column outside the panel
+            const double gc = colmax(c, j, jr), gr = colmax(c, jr, j);
+            if (tid == jr) { colX[1] = pget(0, jr); if (r > cand) colX[2] = pget(0, j); }
+            if (tid == j && r < cand) colX[2] = pget(0, jr);
+            __syncthreads();
+            const double a = ajj, b = colX[2], e = colX[1];
+            __syncthreads();
+            const double det = a * e - b * b;
+            if (det != 0.0) {
+                const double lim = fabs(det) / A.u;
+                if (fabs(e) * gc + fabs(b) * gr <= lim && fabs(b) * gc + fabs(a) * gr <= lim) return false;  // 2x2
+            }
+        }
+        return false;
+    };
+    int cend = np;
+    for (;;) {  // one call site each: the panel stays in registers
+        cend = steps(cend);
+        if constexpr (SEARCH) {
+            if (cend >= ncol || !search(cend)) break;
+        } else {
+            break;
+        }
+    }
+    // the panel back to the front (lower part, un-normalised): pivoted columns and the panel's later
+    // columns (current: the trailing update starts after the panel, at k0 + NB)
 #pragma unroll
     for (int s = 0; s < S; ++s) {
         const int r = k0 + tid + T * s;
@@ -3150,7 +3294,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         double* row = st.F + (int64_t)r * m + k0;
 #pragma unroll
         for (int c = 0; c < NB; ++c)
-            if (c >= cw0 && c < cend && r >= k0 + c) row[c] = P[s][c];
+            if (c >= cw0 && r >= k0 + c) row[c] = P[s][c];
     }
     for (int c = cw0 + tid; c < cend; c += T) piv[k0 + c] = PIV_1X1;
     const int k = k0 + cend;
@@ -3161,6 +3305,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         SF.k1 = k;
         SF.k = k;
         SF.done = k >= p;
+        SF.pad = min(k0 + NB, m);  // first row / column of the trailing update (the panel is current)
         A.big[f] = SF;
     }
 }
@@ -3176,7 +3321,8 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
     const int k0 = S.k0, k1 = S.k1;
     if (k1 <= k0) return;
     const int m = A.fm[f];
-    const int nt = (m - k1 + 63) / 64;
+    const int u0 = S.pad > k1 ? S.pad : k1;  // k_big_panel_reg writes its whole panel back: the update starts after it
+    const int nt = (m - u0 + 63) / 64;
     if ((int)blockIdx.x >= nt * (nt + 1) / 2) return;
     int ti, tj;
     tri_rc((int)blockIdx.x, ti, tj);
@@ -3191,12 +3337,12 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
     }
     __syncthreads();
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    const int i0 = k1 + 64 * ti + 16 * w;
+    const int i0 = u0 + 64 * ti + 16 * w;
     const int lr = lane & 15, lk = lane >> 4;
     dbl4 acc[4];
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
-        const int j0 = k1 + 64 * tj + 16 * c;
+        const int j0 = u0 + 64 * tj + 16 * c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = i0 + lk + 4 * r, j = j0 + lr;
@@ -3216,7 +3362,7 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (diag && c > w) continue;  // wave-uniform: strip entirely above the diagonal
-            const int jb = k1 + 64 * tj + 16 * c + lr;  // B-operand column of this lane
+            const int jb = u0 + 64 * tj + 16 * c + lr;  // B-operand column of this lane
             const double b = (qq < np && jb < m) ? st.at(jb, k0 + qq) : 0.0;
             acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
         }
@@ -3224,7 +3370,7 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
         if (diag && c > w) continue;
-        const int j0 = k1 + 64 * tj + 16 * c;
+        const int j0 = u0 + 64 * tj + 16 * c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = i0 + lk + 4 * r, j = j0 + lr;
@@ -3632,7 +3778,8 @@ hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count
     else if (mmax <= 256) hipLaunchKernelGGL((k_big_panel_reg<1, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
     else if (mmax <= 512) hipLaunchKernelGGL((k_big_panel_reg<2, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
     else if (mmax <= 1024) hipLaunchKernelGGL((k_big_panel_reg<4, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
-    else hipLaunchKernelGGL((k_big_panel_reg<8, 8, 512>), dim3(count), dim3(512), 0, s, A, fronts);
+    else if (mmax <= 2048) hipLaunchKernelGGL((k_big_panel_reg<4, 8, 512>), dim3(count), dim3(512), 0, s, A, fronts);
+    else hipLaunchKernelGGL((k_big_panel_reg<8, 8, 512, false>), dim3(count), dim3(512), 0, s, A, fronts);
     const int nt = (mmax + 63) / 64;
     hipLaunchKernelGGL(k_big_update, dim3(nt * (nt + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
     return hipGetLastError();
