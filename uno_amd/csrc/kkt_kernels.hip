@@ -3034,14 +3034,14 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
             if (!(aak > thres) || A.u * g > aak) return c;  // uniform: the quick 1x1 test failed
             const double dinv = 1.0 / akk;
             minpiv = fmin(minpiv, aak);
-            double w[NB];
+            double l[S];
 #pragma unroll
-            for (int j = c + 1; j < NB; ++j) w[j] = colk[buf][j];
+            for (int s = 0; s < S; ++s) l[s] = P[s][c] * dinv;
 #pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const double l = P[s][c] * dinv;
+            for (int j = c + 1; j < NB; ++j) {  // column operand from LDS (broadcast), one at a time
+                const double wj = colk[buf][j];
 #pragma unroll
-                for (int j = c + 1; j < NB; ++j) P[s][j] -= l * w[j];
+                for (int s = 0; s < S; ++s) P[s][j] -= l[s] * wj;
             }
             if (tid == 0) {  // pivot kinds are stored after the loop (a global store here would be waited for
                              // by the next step's barrier)
