@@ -142,6 +142,39 @@ def test_device_symv_and_quadratic_product():
 
 
 @pytest.mark.gpu
+def test_device_symv_long_rows():
+    """Rows with more than 2048 entries (the arrowband's 6 dense rows carry m = 25 000 Jacobian entries
+    each here) take the chunked reduction (k_symv_long + k_symv_long_fin); the product and the quadratic
+    form agree with the COO product, and two calls give bit-identical results (fixed chunk order)."""
+    import torch
+    import uno_amd
+    n, nv, m, r, c, v, b = uno_amd.arrowband(100000, uno_amd.SEEDS["C2"])
+    g = uno_amd.HipKKT(0)
+    g.analyze(n, r, c)
+    g.factorize(v)
+    g.inertia()
+    rng = np.random.default_rng(5)
+    x, w = rng.standard_normal(n), rng.standard_normal(n)
+    X = torch.from_numpy(x).cuda()
+    W = torch.from_numpy(w).cuda()
+    ys = []
+    for _ in range(2):
+        Y = torch.zeros(n, dtype=torch.float64, device="cuda")
+        torch.cuda.synchronize()
+        g.symv(X.data_ptr(), Y.data_ptr())
+        torch.cuda.synchronize()
+        ys.append(Y.cpu().numpy())
+    np.testing.assert_array_equal(ys[0], ys[1])
+    ref = uno_amd.coo_symv(n, r, c, v, x)  # the generator's C COO product (same as ipm_oracle.symv)
+    scale = uno_amd.coo_symv(n, r, c, np.abs(v), np.abs(x))
+    assert (np.abs(ys[0] - ref) <= 1e-13 * scale + 1e-300).all()
+    dense = np.argsort(-np.abs(scale))[:6]  # the long rows dominate |A||x|
+    assert np.all(np.abs(ref[dense]) > 0.0)
+    q = g.quadratic_product(W.data_ptr(), X.data_ptr())
+    assert abs(q - w @ ref) <= 1e-12 * abs(np.abs(w) @ scale)
+
+
+@pytest.mark.gpu
 def test_device_barrier_diagonal_bitwise():
     """Sigma on the device (uno_kkt_assemble_barrier) equals the host expression of
     PrimalDualInteriorPointProblem.cpp:62-77 bit for bit: 0 + zl / (x - lb) [finite lb] + zu / (x - ub)
