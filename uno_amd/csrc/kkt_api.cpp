@@ -151,7 +151,9 @@ struct uno_kkt {
     DBuf<BigFrontState> big;              // large-front factorization state (fronts with m > kMaxLdsFront)
     DBuf<int32_t> big_pending;
     int32_t* h_big = nullptr;             // pinned: fronts still factoring (run_big_fronts)
-    DBuf<unsigned long long> anorm, counters, stamps, fcnt, minbits;
+    DBuf<unsigned long long> counters, stamps, fcnt;  // counters: kCounterSlots (minbits, anorm inside)
+    unsigned long long* minbits_p = nullptr;  // counters.p + 8
+    unsigned long long* anorm_p = nullptr;    // counters.p + 9
     DBuf<double> fmin;
     int want_stamps = 0;
     DBuf<int32_t> perm_d, cptr, rptr, rslot, long_rows, fparent, delayed, rowpartner;
@@ -632,9 +634,9 @@ int dist_scale(uno_kkt_t h, ScanArgs SA) {
     SA.out = h->rowsum.p;
     HIPCHK(h, launch_rowscan(SA, 2, s));
     if ((rc = top_pass(2, h->rowsum.p, RedOp::SumF64)) != UNO_KKT_OK) return rc;
-    HIPCHK(h, launch_normmax(h->rowsum.p, D.own_orig.p, D.n_own, h->anorm.p, s));
-    HIPCHK(h, launch_normmax(h->rowsum.p, D.top_orig.p, nt, h->anorm.p, s));
-    HIPCHK(h, h->comm->allreduce(h->anorm.p, 1, RedOp::MaxU64, s));
+    HIPCHK(h, launch_normmax(h->rowsum.p, D.own_orig.p, D.n_own, h->anorm_p, s));
+    HIPCHK(h, launch_normmax(h->rowsum.p, D.top_orig.p, nt, h->anorm_p, s));
+    HIPCHK(h, h->comm->allreduce(h->anorm_p, 1, RedOp::MaxU64, s));
     return UNO_KKT_OK;
 }
 
@@ -683,7 +685,7 @@ int sync_and_verify(uno_kkt_t h) {
             if (h->use_front_sweeps) HIPCHK(h, launch_rowsum_norm_orig(h->scan, h->rowsum.p, h->stream));
             else HIPCHK(h, launch_rowsum_norm(h->scan, h->rowsum.p, h->stream));
         }
-        HIPCHK(h, hipMemcpyAsync(h->h_counters + 9, h->anorm.p, 8, hipMemcpyDeviceToHost, h->stream));
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 9, h->anorm_p, 8, hipMemcpyDeviceToHost, h->stream));
         HIPCHK(h, hipStreamSynchronize(h->stream));
         h->norm_valid = true;
         memcpy(&anorm, h->h_counters + 9, 8);
@@ -1034,7 +1036,6 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->fcnt.alloc(S.nf));
     HIPCHK(h, h->fmin.alloc(S.nf));
     if (S.nf > 0) HIPCHK(h, hipMemsetAsync(h->fmin.p, 0x7f, sizeof(double) * S.nf, s));  // 1.4e306: above any threshold
-    if (!h->minbits.p) HIPCHK(h, h->minbits.alloc(1));
     HIPCHK(h, h->perm_d.upload(S.perm, s));
     HIPCHK(h, h->cptr.upload(S.cptr, s));
     HIPCHK(h, h->rptr.upload(S.rptr, s));
@@ -1112,9 +1113,10 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->frow.alloc(S.rows.size()));
     HIPCHK(h, h->fpos.alloc(S.rows.size()));
     HIPCHK(h, h->piv.alloc(S.rows.size()));
-    if (!h->anorm.p) {
-        HIPCHK(h, h->anorm.alloc(1));
-        HIPCHK(h, h->counters.alloc(8));
+    if (!h->counters.p) {
+        HIPCHK(h, h->counters.alloc(kCounterSlots));
+        h->minbits_p = h->counters.p + 8;
+        h->anorm_p = h->counters.p + 9;
     }
     if (S.nf > 0) {  // fronts another rank factors keep zero records
         HIPCHK(h, hipMemsetAsync(h->fstat.p, 0, sizeof(int32_t) * S.nf, s));
@@ -1156,8 +1158,7 @@ int upload_structure(uno_kkt_t h) {
 int enqueue_factorization(uno_kkt_t h) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
-    HIPCHK(h, hipMemsetAsync(h->counters.p, 0, 8 * sizeof(unsigned long long), s));
-    HIPCHK(h, hipMemsetAsync(h->anorm.p, 0, sizeof(unsigned long long), s));
+    HIPCHK(h, launch_reset_counters(h->counters.p, s));  // counters, minbits, anorm
     if (h->use_front_sweeps) {
         // k_pack runs inside launch_front_sweeps (timed with the scaling)
     } else {
@@ -1175,7 +1176,7 @@ int enqueue_factorization(uno_kkt_t h) {
         ScanArgs SA;
         SA.n = S.n; SA.list = nullptr; SA.perm = h->perm_d.p; SA.cptr = h->cptr.p; SA.rptr = h->rptr.p;
         SA.rslot = h->rslot.p; SA.ent_r = h->ent_r.p; SA.ent_c = h->ent_c.p; SA.uval = h->uval.p;
-        SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm.p; SA.long_rows = h->long_rows.p;
+        SA.scale = h->scale.p; SA.out = nullptr; SA.anorm = h->anorm_p; SA.long_rows = h->long_rows.p;
         SA.n_long = h->n_long; SA.max_long = h->max_long; SA.long_chunks = h->long_chunks; SA.part = h->long_part.p;
         SA.uvalR = h->uvalR.p; SA.rowpartner = h->rowpartner.p; SA.long_cnt = h->long_cnt.p;
         SA.scale_out = h->rmax.p;  // scratch of the double-buffered sweeps (new numbering); final scaling after them
@@ -1219,7 +1220,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
     A.ch_cm = h->ch_cm.p; A.ch_relmap_off = h->ch_relmap_off.p; A.ch_cb_off = h->ch_cb_off.p;
-    A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm.p;
+    A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm_p;
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
@@ -1302,15 +1303,14 @@ int enqueue_factorization(uno_kkt_t h) {
             }
         }
     }
-    HIPCHK(h, hipMemsetAsync(h->minbits.p, 0xff, 8, s));
-    HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits.p, s));
+    HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits_p, s));
     if (h->world > 1) {
         // counters[7] keeps this rank's delayed-column count; 0..6 are summed over the ranks
         HIPCHK(h, hipMemcpyAsync(h->counters.p + 7, h->counters.p + 6, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
         HIPCHK(h, h->comm->allreduce(h->counters.p, 7, RedOp::SumU64, s));
     }
-    HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipMemcpyAsync(h->h_counters + 8, h->minbits.p, 8, hipMemcpyDeviceToHost, s));
+    // counters and minbits in one copy (h_counters[8] is the min pivot bits)
+    HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     h->factor_enqueued = true;
     h->df_rx_valid = false;  // pivoting may have permuted rows
     return UNO_KKT_OK;
@@ -1877,7 +1877,7 @@ int uno_kkt_debug_scaling(uno_kkt_t h, double* scale, double* anorm) {
     }
     if (h->S.n > 0) HIPCHK(h, hipMemcpy(scale, h->scale.p, sizeof(double) * h->S.n, hipMemcpyDeviceToHost));
     unsigned long long b = 0;
-    HIPCHK(h, hipMemcpy(&b, h->anorm.p, sizeof(b), hipMemcpyDeviceToHost));
+    HIPCHK(h, hipMemcpy(&b, h->anorm_p, sizeof(b), hipMemcpyDeviceToHost));
     memcpy(anorm, &b, sizeof(b));
     return UNO_KKT_OK;
 }

@@ -3725,6 +3725,17 @@ hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, co
     return hipGetLastError();
 }
 
+// one launch for the per-factorization resets: counters[0..7] = 0, minbits (slot 8) = all ones (the min
+// is taken on the bit patterns), anorm (slot 9) = 0 -- three fill launches before
+__global__ void k_reset_counters(unsigned long long* __restrict__ c) {
+    const int t = threadIdx.x;
+    if (t < kCounterSlots) c[t] = t == 8 ? ~0ull : 0ull;
+}
+hipError_t launch_reset_counters(unsigned long long* counters, hipStream_t s) {
+    hipLaunchKernelGGL(k_reset_counters, dim3(1), dim3(64), 0, s, counters);
+    return hipGetLastError();
+}
+
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s) {
     if (n == 0) return hipSuccess;
     hipLaunchKernelGGL(k_rhs_scale, dim3(grid_for(n, 256)), dim3(256), 0, s, b, scale, w, n);

@@ -219,6 +219,9 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
 // counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
                         unsigned long long* counters, unsigned long long* minbits, hipStream_t s);
+// the factorization's device counter block: [0..7] pivot counters, [8] min pivot bits, [9] ||A_pre||_inf bits
+constexpr int kCounterSlots = 10;
+hipError_t launch_reset_counters(unsigned long long* counters, hipStream_t s);
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
