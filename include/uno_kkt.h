@@ -93,7 +93,9 @@ int uno_kkt_factorize(uno_kkt_t handle, const double* values, int values_on_devi
  * inertia-correction loop (PrimalDualRegularization.hpp:178-179, 210-211) rewrites only the regularization
  * diagonal, which COOFormat stores first (COOFormat.hpp:102-110), so each retry moves reg_size doubles
  * instead of nnz.  Options: "pin_host_values" (1: the host buffer is page-locked once with hipHostRegister,
- * so uploads are direct DMA; it must stay allocated while the handle uses it). */
+ * so uploads are direct DMA; a registration is keyed by pointer and length, and the buffer must stay
+ * allocated until the caller passes another buffer to uno_kkt_factorize, re-analyses or destroys the handle,
+ * each of which unregisters it). */
 int uno_kkt_factorize_update(uno_kkt_t handle, const double* values, int64_t first, int64_t count);
 
 /* Device-side value edits between factorizations (the inertia-correction loop changes only the
@@ -208,6 +210,11 @@ typedef struct {
     int64_t top_rows;      /* rows eliminated in top fronts */
     double my_flops, top_flops;
     double est_imbalance;  /* max rank work / mean rank work (analysis estimate) */
+    int64_t partitioned;   /* 1: the factorization is split over the ranks; 0: the partition was declined
+                              (fewer subtrees than ranks, or est_efficiency below option "dist_min_efficiency",
+                              default 0.5; option "dist_force" = 1 overrides): every rank factors and solves
+                              the whole matrix itself (replicas, no collective), so every rank's x is complete */
+    double est_efficiency; /* total work / (world * (max rank work + top work)), analysis cost model */
 } uno_kkt_dist_info_t;
 int uno_kkt_dist_info(uno_kkt_t handle, uno_kkt_dist_info_t* info);
 

@@ -14,6 +14,11 @@ extern "C" {
  * -nf if cap is too small, -1 on a bad pattern. */
 int64_t uno_kkt_debug_partition(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int world,
                                 int32_t* owner, int32_t* parent, int64_t cap, int64_t* n_subtrees);
+/* The multi-GPU gate of uno_kkt_analyze (host only): 1 if a group of `world` ranks would partition the
+ * factorization (at least `world` subtrees and estimated efficiency >= min_efficiency), 0 if it would run
+ * replicas; -1 on a bad pattern.  efficiency / n_subtrees (optional) receive the estimate. */
+int uno_kkt_debug_partition_gate(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int world,
+                                 double min_efficiency, double* efficiency, int64_t* n_subtrees);
 /* Host-only symbolic analysis: per front its order, fully-summed columns and assembly-tree level. */
 int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int32_t* front_order,
                              int32_t* front_pivots, int32_t* front_level, int64_t cap);

@@ -144,7 +144,7 @@ def test_distributed_delayed_pivots(ua):
         o.analyze(nn, rr, cc)
         o.factorize(vv)
         b = rng.standard_normal(nn)
-        out = run_group(ua, 2, nn, rr, cc, (vv,), b)
+        out = run_group(ua, 2, nn, rr, cc, (vv,), b, dist_force=1)  # small: split although the gate would decline
         expect = (int((ev > 0).sum()), int((ev < 0).sum()), 0)
         assert out[0][0][0][0] == out[1][0][0][0] == o.inertia() == expect
         x = out[0][0][0][1]
@@ -216,3 +216,89 @@ def test_multiprocess_host_transport(world):
         assert run["rel_residual"] < RES_TOL
         assert run["max_rel_diff"] < 1e-9
     assert r0["stats"]["factorizations"] == 2 and r0["stats"]["solves"] == 2
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("aborting_rank", [0, 1])
+def test_distributed_abort_on_one_rank(ua, aborting_rank):
+    """a dataflow-solve abort on ONE rank only.  The abort flag is all-reduced before any rank
+    writes x, so no rank writes x from a peer's invalid top values, and every rank redoes the solve level by
+    level; with x aliasing the rhs (in-place device solve) the redo still starts from b.  Rank 0's gathered
+    solution equals the single-GPU one."""
+    import torch
+    n, nv, m, r, c, v, b = ua.arrowband(40000, ua.SEEDS["C2"])
+    single = ua.HipKKT(0)
+    single.analyze(n, r, c)
+    single.factorize(v)
+    ref = single.solve(b)
+    world = 2
+    group = ua.LocalGroup(world)
+    out, errs = [None] * world, []
+
+    def rank_main(q):
+        try:
+            g = ua.HipKKT(0, dist_dataflow_solve=1)
+            g.attach_local(group, q)
+            g.analyze(n, r, c)
+            g.factorize(v)
+            g.inertia()
+            if q == aborting_rank:
+                g.set_option("debug_abort_solves", 1)
+            bd = torch.from_numpy(b.copy()).to("cuda")
+            g.solve_device(bd.data_ptr(), bd.data_ptr())
+            torch.cuda.synchronize()
+            out[q] = (bd.cpu().numpy(), g.stats())
+            g.close()
+        except Exception as e:  # surfaced below
+            errs.append((q, repr(e)))
+
+    th = [threading.Thread(target=rank_main, args=(q,)) for q in range(world)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    group.close()
+    assert not errs, errs
+    assert all(o[1]["solve_aborts"] == 1 for o in out)  # every rank saw the all-reduced verdict
+    np.testing.assert_allclose(out[0][0], ref, rtol=1e-12, atol=1e-14 * np.abs(ref).max())
+
+
+def test_partition_gate_cpu(ua):
+    """SURVEY.md 8(e) / north_star gate, host only: the arrowband family exposes enough balanced subtrees, so
+    world ranks partition it (estimated efficiency >= 0.5); a dense system (one front) and a tiny chain
+    expose too little, so the group declines and runs replicas."""
+    n, _, _, r, c, _, _ = ua.arrowband(60000, ua.SEEDS["C3"])
+    for world in (2, 4, 8):
+        ok, eff, nsub = ua.debug_partition_gate(n, r, c, world)
+        assert ok and eff >= 0.5 and nsub >= world, (world, eff, nsub)
+    k = 120  # dense: one front, no independent subtrees
+    rr, cc = np.tril_indices(k)
+    ok, eff, nsub = ua.debug_partition_gate(k, rr, cc, 4)
+    assert not ok and nsub < 4
+    rr = np.arange(1, 200)  # a path of 200 nodes: separators of 1 node, but little work to split
+    ok8, eff8, _ = ua.debug_partition_gate(200, np.concatenate([np.arange(200), rr]),
+                                           np.concatenate([np.arange(200), rr - 1]), 8, min_efficiency=0.99)
+    assert not ok8 and eff8 < 0.99
+
+
+@pytest.mark.gpu
+def test_declined_partition_runs_replicas(ua):
+    """The declined outcome on the GPU: a dense indefinite system in a 2-rank in-process group is not split
+    (dist_info partitioned == 0); every rank factors and solves the whole matrix itself, so every rank's
+    inertia and solution equal the single-GPU ones, with no collective on the data path."""
+    rng = np.random.default_rng(3)
+    k = 150
+    M = rng.standard_normal((k, k))
+    S = M + M.T
+    rr, cc = np.tril_indices(k)
+    vv = S[rr, cc]
+    b = rng.standard_normal(k)
+    single = ua.HipKKT(0)
+    single.analyze(k, rr, cc)
+    single.factorize(vv)
+    ine, x = single.inertia(), single.solve(b)
+    out = run_group(ua, 2, k, rr, cc, (vv,), b)
+    for q in range(2):
+        assert out[q][1]["partitioned"] == 0
+        assert out[q][0][0][0] == ine
+        np.testing.assert_array_equal(out[q][0][0][1], x)

@@ -359,3 +359,30 @@ def test_factorize_update_prefix(uno_amd):
         np.testing.assert_array_equal(g.solve(b), full.solve(b))
     with pytest.raises(RuntimeError):
         g.factorize_update(vals, n - 1, len(vals))  # range beyond the array
+
+
+def test_dataflow_abort_redone_and_rearmed(uno_amd):
+    """A dataflow solve whose dependency waits give up (forced here: option debug_abort_solves starts the
+    walk with its abort flag set) is redone level by level within the same call -- same solution, bit for
+    bit, also for an aliasing device solve -- and the dataflow solve stays armed for the next solve
+    (one abort used to disable it for the handle's lifetime)."""
+    import torch
+    from uno_amd import HipKKT, arrowband, SEEDS
+    N, nv, m, r, c, v, b = arrowband(20000, SEEDS["C2"])
+    g, ref = HipKKT(0), HipKKT(0, dataflow_solve=0)
+    for h in (g, ref):
+        h.analyze(N, r, c)
+        h.factorize(v)
+    x_ref = ref.solve(b)
+    g.set_option("debug_abort_solves", 1)
+    np.testing.assert_array_equal(g.solve(b), x_ref)
+    st = g.stats()
+    assert st["solve_aborts"] == 1 and st["solve_grid"] > 0  # redone, and still armed
+    g.set_option("debug_abort_solves", 1)
+    bd = torch.from_numpy(b.copy()).to("cuda")
+    g.solve_device(bd.data_ptr(), bd.data_ptr())  # x aliases the rhs: the redo must still see b
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(bd.cpu().numpy(), x_ref)
+    np.testing.assert_array_equal(g.solve(b), x_ref)  # a normal dataflow solve again
+    st = g.stats()
+    assert st["solve_aborts"] == 2 and st["solve_grid"] > 0

@@ -6,4 +6,4 @@ surface used by the tests and bench.py.
 """
 from .kkt import (HipKKT, HipLDLSolver, KKTError, SparseSymmetricMatrix, UnstableRegularization,  # noqa: F401
                   arrowband, coo_symv, load_library, regularize_augmented_matrix, SEEDS,
-                  LocalGroup, GlooComm, rccl_unique_id, debug_partition)
+                  LocalGroup, GlooComm, rccl_unique_id, debug_partition, debug_partition_gate)

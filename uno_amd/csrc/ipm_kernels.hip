@@ -192,8 +192,9 @@ __global__ void k_symv_long_fin(SymvArgs A) {
     if (A.dot_w) A.dot_part[i] = A.dot_w[oi] * acc;
 }
 
-// sum of per-row partials (quadratic_product): one block-sum per workgroup, atomics on one double
-__global__ void k_sum(const double* __restrict__ v, int64_t n, double* __restrict__ out) {
+// sum of per-row partials (quadratic_product), deterministic: pass 1 writes one block-sum per workgroup
+// (fixed grid, fixed tree order inside the block), pass 2 (one block) sums them in block order
+__global__ void k_sum(const double* __restrict__ v, int64_t n, double* __restrict__ part) {
     __shared__ double red[kT / 64];
     double s = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) s += v[i];
@@ -202,7 +203,20 @@ __global__ void k_sum(const double* __restrict__ v, int64_t n, double* __restric
     __syncthreads();
     if (threadIdx.x == 0) {
         for (int w = 1; w < kT / 64; ++w) s += red[w];
-        atomicAdd(out, s);
+        part[blockIdx.x] = s;
+    }
+}
+
+__global__ void k_sum_fin(const double* __restrict__ part, int nparts, double* __restrict__ out) {
+    __shared__ double red[kT / 64];
+    double s = 0.0;
+    for (int i = threadIdx.x; i < nparts; i += kT) s += part[i];
+    for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < kT / 64; ++w) s += red[w];
+        *out = s;
     }
 }
 
@@ -259,10 +273,10 @@ hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s) {
         hipLaunchKernelGGL(k_symv_long, dim3((unsigned)A.long_chunks, (unsigned)A.n_long), dim3(kT), 0, s, A);
         hipLaunchKernelGGL(k_symv_long_fin, dim3((unsigned)((A.n_long + 63) / 64)), dim3(64), 0, s, A);
     }
-    if (A.dot_w) {
-        hipError_t e = hipMemsetAsync(dot_out, 0, sizeof(double), s);
-        if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_sum, dim3(grid_of(A.n) > 1024 ? 1024 : grid_of(A.n)), dim3(kT), 0, s, A.dot_part, A.n, dot_out);
+    if (A.dot_w) {  // dot_out: 1 + kSumParts doubles (result, then the block partials)
+        const int g = (int)(grid_of(A.n) > kSumParts ? kSumParts : grid_of(A.n));
+        hipLaunchKernelGGL(k_sum, dim3(g), dim3(kT), 0, s, A.dot_part, A.n, dot_out + 1);
+        hipLaunchKernelGGL(k_sum_fin, dim3(1), dim3(kT), 0, s, dot_out + 1, g, dot_out);
     }
     return hipGetLastError();
 }

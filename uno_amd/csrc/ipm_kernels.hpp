@@ -44,12 +44,14 @@ struct SymvArgs {
     double* long_part = nullptr;         // n_long * long_chunks chunk partials (summed in chunk order)
 };
 constexpr int kSymvChunk = 4096;
+constexpr int kSumParts = 1024;  // quadratic_product: block partials of the deterministic two-pass sum
 
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
                       const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s);
 hipError_t launch_direction(const DirArgs& A, hipStream_t s);
 hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double* lb, const double* ub, const double* x,
                           const double* zl, const double* zu, int64_t count, double* values, hipStream_t s);
+// dot_out (only with A.dot_w): 1 + kSumParts doubles, the result first
 hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s);
 
 }  // namespace ukkt

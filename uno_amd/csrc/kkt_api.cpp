@@ -193,6 +193,8 @@ struct uno_kkt {
     uint32_t df_epoch = 0;
     bool df_rx_valid = false;      // rxpos matches the last factorization's pivoting
     int64_t df_aborts = 0;
+    int df_consec_aborts = 0;      // consecutive aborted dataflow solves (kMaxDfAborts turns the walk off)
+    int debug_abort_solves = 0;    // option debug_abort_solves: the next k dataflow solves start with the abort flag set (tests)
     DBuf<int32_t> df_order, df_desc, df_xpos, df_rxpos;
     DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
     DBuf<uint32_t> df_cnt, df_done, df_abort;
@@ -225,11 +227,17 @@ struct uno_kkt {
     int pin_host = 0;                     // option pin_host_values
     int mfma_fronts = 0;                  // option mfma_fronts: one-wave fronts on the matrix-core tile kernels
     const double* pinned_ptr = nullptr;   // caller buffer registered with hipHostRegister
+    size_t pinned_bytes = 0;
     DBuf<int64_t> edit_pos;               // uno_kkt_set_values staging
     DBuf<double> edit_val;
     bool packed_valid = false;            // uval holds the current values (symv reuses the factor's pack)
     ukkt::Transport* comm = nullptr;
-    int rank = 0, world = 1;
+    int rank = 0, world = 1;      // effective: world 1 when the partition was declined (every rank a replica)
+    int comm_rank = 0, comm_world = 1;  // the attached transport's
+    bool dist_declined = false;   // analysis found too little top-level parallelism (SURVEY.md 8(e) gate)
+    double dist_efficiency = 0.0; // estimated parallel efficiency of the partition (analysis cost model)
+    double dist_min_eff = 0.5;    // option dist_min_efficiency
+    int dist_force = 0;           // option dist_force: partition whatever the estimate (tests, experiments)
     int gather_solution = 1;
     DistState dist;
     uno_kkt_stats_t st{};
@@ -349,15 +357,23 @@ DfArgs dataflow_args(uno_kkt_t h) {
 }
 
 // After the stream has drained: a dataflow solve whose waits hit their limit produced no valid
-// solution (k_xs_out then leaves x untouched); the flag is cleared and the level schedule is used from
-// then on.  Returns true if the solve aborted.
+// solution (k_xs_out then leaves x untouched); the flag is cleared, the caller redoes that one solve with
+// the level schedule and the dataflow solve stays armed for the next one.  Only a run of kMaxDfAborts
+// consecutive aborts (a grid that cannot be resident, e.g. ranks sharing one GPU) turns it off for the
+// handle.  Returns true if the solve aborted.
+constexpr int kMaxDfAborts = 3;
 bool dataflow_aborted(uno_kkt_t h) {
     uint32_t ab = 0;
     memcpy(&ab, h->h_counters + 10, sizeof(ab));
-    if (ab == 0) return false;
+    if (ab == 0) {
+        h->df_consec_aborts = 0;
+        return false;
+    }
     h->df_aborts++;
-    h->df_enabled = 0;
-    h->df_grid = 0;
+    if (++h->df_consec_aborts >= kMaxDfAborts) {
+        h->df_enabled = 0;
+        h->df_grid = 0;
+    }
     memset(h->h_counters + 10, 0, 8);
     return true;
 }
@@ -1411,6 +1427,9 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
+    else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
+    else if (n == "dist_min_efficiency") h->dist_min_eff = value;
+    else if (n == "dist_force") h->dist_force = value != 0.0;
     else if (n == "dataflow_factor") {
         h->dff_enabled = std::max(0, std::min(2, (int)value));
         if (h->analyzed) {
@@ -1455,6 +1474,29 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
     auto t0 = std::chrono::steady_clock::now();
     std::string msg = ukkt::analyze(n, nnz, row, col, h->aopt, h->P, h->S);
     if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
+    // multi-GPU gate (north_star: partition "only when the ordering exposes enough top-level
+    // parallelism"): the subtree partition is used only if it has at least `world` subtrees and its estimated
+    // parallel efficiency total / (world * (max rank work + top work)) reaches dist_min_efficiency; otherwise
+    // every rank factors and solves the whole matrix on its own GPU (replicas, no collective).  The decision
+    // is a pure function of the pattern, so every rank takes the same one; delayed-pivot rebuilds keep it.
+    h->world = h->comm_world;
+    h->rank = h->comm_rank;
+    h->dist_declined = false;
+    h->dist_efficiency = 0.0;
+    if (h->world > 1) {
+        Partition Pt;
+        partition_tree(h->S, h->world, Pt);
+        const double denom = (double)h->world * (Pt.max_rank_work + Pt.top_work);
+        h->dist_efficiency = denom > 0.0 ? Pt.total_work / denom : 0.0;
+        if (!h->dist_force && (Pt.n_subtrees < h->world || h->dist_efficiency < h->dist_min_eff)) {
+            h->dist_declined = true;
+            h->world = 1;
+            h->rank = 0;
+            if (h->verbose)
+                fprintf(stderr, "[uno_kkt] partition declined: %lld subtrees for %d ranks, efficiency %.3f < %.3f: replicas\n",
+                        (long long)Pt.n_subtrees, h->comm_world, h->dist_efficiency, h->dist_min_eff);
+        }
+    }
     HIPCHK(h, h->values.alloc(nnz));
     int rc = upload_structure(h);
     if (rc != UNO_KKT_OK) return rc;
@@ -1482,11 +1524,25 @@ int uno_kkt_set_values(uno_kkt_t h, const int64_t* positions, const double* v, i
     }
     h->packed_valid = false;
     if (count == 0) return UNO_KKT_OK;
+    // a position listed twice keeps its LAST value (the sequential-copy semantics): duplicates are resolved
+    // here, so the parallel scatter below writes every position once
+    std::vector<int64_t> order((size_t)count);
+    for (int64_t i = 0; i < count; ++i) order[i] = i;
+    std::stable_sort(order.begin(), order.end(), [&](int64_t a, int64_t b) { return positions[a] < positions[b]; });
+    std::vector<int64_t> upos;
+    std::vector<double> uv;
+    for (int64_t q = 0; q < count; ++q) {
+        const int64_t i = order[q];
+        if (q + 1 < count && positions[order[q + 1]] == positions[i]) continue;  // a later edit of the same position wins
+        upos.push_back(positions[i]);
+        uv.push_back(v[i]);
+    }
+    count = (int64_t)upos.size();
     // one H2D copy of (positions, values), one scatter kernel
     HIPCHK(h, h->edit_pos.alloc(count));
     HIPCHK(h, h->edit_val.alloc(count));
-    HIPCHK(h, hipMemcpyAsync(h->edit_pos.p, positions, sizeof(int64_t) * count, hipMemcpyHostToDevice, h->stream));
-    HIPCHK(h, hipMemcpyAsync(h->edit_val.p, v, sizeof(double) * count, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->edit_pos.p, upos.data(), sizeof(int64_t) * count, hipMemcpyHostToDevice, h->stream));
+    HIPCHK(h, hipMemcpyAsync(h->edit_val.p, uv.data(), sizeof(double) * count, hipMemcpyHostToDevice, h->stream));
     HIPCHK(h, launch_scatter64(h->edit_val.p, h->edit_pos.p, const_cast<double*>(h->values_ptr), count, h->stream));
     HIPCHK(h, hipStreamSynchronize(h->stream));  // the host arrays may be reused on return
     return UNO_KKT_OK;
@@ -1551,9 +1607,13 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     } else {
         // option pin_host_values: the caller's buffer is page-locked once (hipHostRegister) so every later
         // upload is a direct DMA; it is unregistered when the pointer changes or the handle is destroyed
-        if (h->pin_host && S.nnz > 0 && values != h->pinned_ptr) {
+        // (a registration is keyed by pointer AND length: the same address with another pattern size is a
+        // new buffer).  The caller keeps a registered buffer allocated until it passes another pointer, calls
+        // uno_kkt_analyze again or destroys the handle (include/uno_kkt.h).
+        if (h->pin_host && S.nnz > 0 && (values != h->pinned_ptr || h->pinned_bytes != (size_t)S.nnz * sizeof(double))) {
             if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
-            h->pinned_ptr = hipHostRegister(const_cast<double*>(values), S.nnz * sizeof(double), hipHostRegisterDefault) ==
+            h->pinned_bytes = (size_t)S.nnz * sizeof(double);
+            h->pinned_ptr = hipHostRegister(const_cast<double*>(values), h->pinned_bytes, hipHostRegisterDefault) ==
                                     hipSuccess ? values : nullptr;
             (void)hipGetLastError();
         }
@@ -1585,11 +1645,11 @@ int uno_kkt_inertia(uno_kkt_t h, int64_t* positive, int64_t* negative, int64_t* 
 namespace {
 // One solve with the last factorization, device pointers (b may alias xd: b is read by the first kernel,
 // xd written by the last).  Returns after the stream has drained when the dataflow solve ran (its abort
-// flag is checked in the same call).
-int solve_core(uno_kkt_t h, const double* b, double* xd) {
+// flag is checked in the same call; an aborted solve is redone with the level schedule, allow_df = false).
+int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
-    const bool df = h->df_enabled && h->df_grid > 0;
+    const bool df = allow_df && h->df_enabled && h->df_grid > 0;
     const bool dist = h->world > 1;
     SolveArgs A;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
@@ -1621,6 +1681,10 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
                                    dist ? h->dist.own_orig.p : nullptr));
         }
         Df.epoch = ++h->df_epoch;
+        if (h->debug_abort_solves > 0) {  // tests: an abort of this rank's walk (its waits give up at once)
+            h->debug_abort_solves--;
+            HIPCHK(h, hipMemsetD32Async(reinterpret_cast<hipDeviceptr_t>(h->df_abort.p), 1, 1, s));
+        }
         if (h->want_solve_stamps) {
             if (h->df_stamps.n != (size_t)(8 * S.nf)) HIPCHK(h, h->df_stamps.alloc(8 * S.nf));
             Df.stamps = h->df_stamps.p;
@@ -1674,6 +1738,23 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
         TimerScope t(h, KC_SOLVE_BWD);
         HIPCHK(h, run(P0, P0.sol[q], false));
     }
+    if (dist && allow_df) {
+        // distributed: the abort flag is all-reduced BEFORE anything writes x (a rank whose walk is empty or
+        // ineligible ran the level schedule and contributes 0), so every rank sees the same verdict, none
+        // writes x from a peer's invalid root / top values (x may alias the rhs), and every rank redoes the
+        // solve if any aborted, keeping the same path through the collectives
+        if (!h->df_abort64.p) HIPCHK(h, h->df_abort64.alloc(1));
+        HIPCHK(h, hipMemsetAsync(h->df_abort64.p, 0, sizeof(unsigned long long), s));
+        if (df) HIPCHK(h, hipMemcpyAsync(h->df_abort64.p, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+        HIPCHK(h, h->comm->allreduce(h->df_abort64.p, 1, RedOp::MaxU64, s));
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort64.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, hipStreamSynchronize(s));
+        if (dataflow_aborted(h)) {
+            if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
+            if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted on some rank: this solve redone level by level\n");
+            return solve_core(h, b, xd, false);
+        }
+    }
     {
         TimerScope t(h, KC_RHS);
         if (df && dist) {  // own rows and top rows (the rows a rank's solution holds)
@@ -1700,26 +1781,15 @@ int solve_core(uno_kkt_t h, const double* b, double* xd) {
         if (h->rank == 0)
             HIPCHK(h, launch_scatter(D.xbuf.p, D.all_own_orig.p, xd, D.all_own_off[h->world], s));
     }
-    if (df || dist) {
-        // a dataflow solve is checked in the same call: on an abort k_xs_out has left x (and so an aliased
-        // rhs) untouched, and the solve is redone with the level schedule.  Distributed: every rank takes
-        // part in the all-reduce of the abort flag (a rank whose walk is empty or ineligible runs the
-        // level schedule and contributes 0), and every rank redoes the solve if any aborted, so the ranks
-        // keep taking the same path through the collectives
-        if (dist) {
-            if (!h->df_abort64.p) HIPCHK(h, h->df_abort64.alloc(1));
-            HIPCHK(h, hipMemsetAsync(h->df_abort64.p, 0, sizeof(unsigned long long), s));
-            if (df) HIPCHK(h, hipMemcpyAsync(h->df_abort64.p, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
-            HIPCHK(h, h->comm->allreduce(h->df_abort64.p, 1, RedOp::MaxU64, s));
-            HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort64.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        } else {
-            HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        }
+    if (df && !dist) {
+        // one GPU: k_xs_out itself skips the write of x on an abort (x may alias the rhs); the flag is read
+        // in the same call and the solve redone with the level schedule
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         HIPCHK(h, hipStreamSynchronize(s));
         if (dataflow_aborted(h)) {
             if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
-            if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: redone level by level\n");
-            return solve_core(h, b, xd);
+            if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: this solve redone level by level\n");
+            return solve_core(h, b, xd, false);
         }
     }
     return UNO_KKT_OK;
@@ -1826,6 +1896,21 @@ int64_t uno_kkt_debug_partition(int64_t n, int64_t nnz, const int64_t* row, cons
     return S.nf;
 }
 
+// diagnostics (include/uno_kkt_debug.h): the multi-GPU gate of uno_kkt_analyze on a pattern (no device)
+int uno_kkt_debug_partition_gate(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int world,
+                                 double min_efficiency, double* efficiency, int64_t* n_subtrees) {
+    Pattern P;
+    Symbolic S;
+    if (!ukkt::analyze(n, nnz, row, col, AnalysisOptions(), P, S).empty()) return -1;
+    Partition Pt;
+    partition_tree(S, world, Pt);
+    const double denom = (double)world * (Pt.max_rank_work + Pt.top_work);
+    const double eff = denom > 0.0 ? Pt.total_work / denom : 0.0;
+    if (efficiency) *efficiency = eff;
+    if (n_subtrees) *n_subtrees = Pt.n_subtrees;
+    return (world > 1 && Pt.n_subtrees >= world && eff >= min_efficiency) ? 1 : 0;
+}
+
 // diagnostics (include/uno_kkt_debug.h): host-only analysis, per front order / pivots / level
 int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const int64_t* col, int32_t* fm, int32_t* fp,
                              int32_t* flevel, int64_t cap) {
@@ -1843,10 +1928,14 @@ int64_t uno_kkt_debug_fronts(int64_t n, int64_t nnz, const int64_t* row, const i
 // diagnostics (include/uno_kkt_debug.h): per-front phase stamps of the last factorization
 int64_t uno_kkt_debug_stamps(uno_kkt_t h, uint64_t* out, int64_t cap, int32_t* fm, int32_t* fp, int32_t* flevel) {
     if (!h || !h->stamps.p) return -1;
-    if (h->factor_enqueued) finish_factorization(h);
+    if (h->factor_enqueued) {
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;  // a device / runtime failure is reported
+    }
     int64_t nf = h->S.nf;
     if (cap < 8 * nf) return -(8 * nf);
-    hipMemcpy(out, h->stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost);
+    if (hipMemcpy(out, h->stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost) != hipSuccess)
+        return set_err(h, UNO_KKT_ERR_HIP, "stamps copy failed");
     for (int64_t f = 0; f < nf; ++f) { fm[f] = h->S.f_m[f]; fp[f] = h->S.f_p[f]; flevel[f] = h->S.f_level[f]; }
     return nf;
 }
@@ -1856,8 +1945,8 @@ int64_t uno_kkt_debug_solve_stamps(uno_kkt_t h, uint64_t* out, int64_t cap) {
     if (!h || !h->df_stamps.p) return -1;
     const int64_t nf = h->S.nf;
     if (cap < 8 * nf) return -(8 * nf);
-    hipStreamSynchronize(h->stream);
-    hipMemcpy(out, h->df_stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost);
+    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipMemcpy(out, h->df_stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost));
     return nf;
 }
 
@@ -2010,7 +2099,7 @@ int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* 
     }
     if (w) {
         if (h->symv_part.n != (size_t)S.n) HIPCHK(h, h->symv_part.alloc(std::max<int64_t>(S.n, 1)));
-        if (!h->dot_d.p) HIPCHK(h, h->dot_d.alloc(1));
+        if (!h->dot_d.p) HIPCHK(h, h->dot_d.alloc(1 + kSumParts));
         A.dot_part = h->symv_part.p;
     }
     {
@@ -2052,8 +2141,8 @@ static int attach(uno_kkt_t h, ukkt::Transport* t) {
     delete h->comm;
     h->comm = t;
     h->own_device = false;
-    h->rank = t->rank();
-    h->world = t->size();
+    h->rank = h->comm_rank = t->rank();
+    h->world = h->comm_world = t->size();
     h->analyzed = h->factored = h->factor_enqueued = false;
     return UNO_KKT_OK;
 }
@@ -2094,8 +2183,10 @@ int uno_kkt_attach_host(uno_kkt_t h, const uno_kkt_host_comm_t* comm, int rank, 
 int uno_kkt_dist_info(uno_kkt_t h, uno_kkt_dist_info_t* out) {
     if (!h || !out) return UNO_KKT_ERR_ARG;
     memset(out, 0, sizeof(*out));
-    out->rank = h->rank;
-    out->world = h->world;
+    out->rank = h->comm_rank;
+    out->world = h->comm_world;
+    out->partitioned = h->analyzed && h->world > 1;
+    out->est_efficiency = h->dist_efficiency;
     if (h->world > 1 && h->analyzed) {
         const DistState& D = h->dist;
         out->subtrees = D.part.n_subtrees;

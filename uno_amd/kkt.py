@@ -55,7 +55,7 @@ class KKTDistInfo(ctypes.Structure):
         ("rank", ctypes.c_int64), ("world", ctypes.c_int64), ("subtrees", ctypes.c_int64),
         ("top_fronts", ctypes.c_int64), ("my_fronts", ctypes.c_int64), ("own_rows", ctypes.c_int64),
         ("top_rows", ctypes.c_int64), ("my_flops", ctypes.c_double), ("top_flops", ctypes.c_double),
-        ("est_imbalance", ctypes.c_double),
+        ("est_imbalance", ctypes.c_double), ("partitioned", ctypes.c_int64), ("est_efficiency", ctypes.c_double),
     ]
 
     def as_dict(self):
@@ -108,6 +108,8 @@ def load_library():
     lib.uno_kkt_debug_partition.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _i64p]
     lib.uno_kkt_debug_partition.restype = ctypes.c_int64
+    lib.uno_kkt_debug_partition_gate.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int, ctypes.c_double,
+                                                 _f64p, _i64p]
     lib.uno_kkt_rhs_setup.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p]
     lib.uno_kkt_assemble_rhs.argtypes = [vp, vp, vp, vp, vp, vp]
     lib.uno_kkt_assemble_direction.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, vp, vp, vp, vp, vp, vp,
@@ -177,8 +179,11 @@ class HipKKT:
             self._check(self.lib.uno_kkt_factorize(self.h, ctypes.c_void_p(int(device_ptr)), 1))
         elif values is not None:
             v, vp = _f64(values)
-            self._v_keep = v
+            # the previous array may still be page-locked by the library (option pin_host_values): it stays
+            # referenced until the call has unregistered it, so it is never freed while registered
+            prev, self._v_keep = getattr(self, "_v_keep", None), v
             self._check(self.lib.uno_kkt_factorize(self.h, v.ctypes.data_as(ctypes.c_void_p), 0))
+            del prev
         else:
             self._check(self.lib.uno_kkt_factorize(self.h, None, 0))
 
@@ -186,7 +191,9 @@ class HipKKT:
         """Refactorize after a host edit of positions [first, first+count) of `values` (the array of the
         previous host factorization): only that range is uploaded."""
         v, _ = _f64(values)
-        self._v_keep = v
+        # the library registers only the buffer of uno_kkt_factorize (kept in self._v_keep); this one is
+        # referenced too, as an asynchronous copy from it may still be in flight
+        self._v_upd = v
         self._check(self.lib.uno_kkt_factorize_update(self.h, v.ctypes.data_as(ctypes.c_void_p), int(first), int(count)))
 
     def fill_values(self, first, count, value):
@@ -402,6 +409,19 @@ def debug_partition(n, rows, cols, world):
     if nf < 0:
         raise KKTError(UNO_KKT_ERR_ARG if nf == -1 else nf, "debug_partition failed")
     return owner[:nf].copy(), parent[:nf].copy(), ns.value
+
+
+def debug_partition_gate(n, rows, cols, world, min_efficiency=0.5):
+    """Host-only: (partition?, estimated efficiency, subtrees) of the multi-GPU gate of uno_kkt_analyze."""
+    lib = load_library()
+    r, rp = _i64(rows)
+    c, cp = _i64(cols)
+    eff, ns = ctypes.c_double(), ctypes.c_int64()
+    rc = lib.uno_kkt_debug_partition_gate(int(n), len(r), rp, cp, int(world), float(min_efficiency), ctypes.byref(eff),
+                                          ctypes.byref(ns))
+    if rc < 0:
+        raise KKTError(UNO_KKT_ERR_ARG, "debug_partition_gate failed")
+    return bool(rc), eff.value, ns.value
 
 
 # ---------------------------------------------------------------------------------------------
