@@ -1,15 +1,37 @@
 """CPU oracle (test infrastructure only) for the device-side vector work around the KKT solve,
 restating the reference loops in the same floating-point order:
 
+- barrier_diagonal         PrimalDualInteriorPointProblem.cpp:56-78 (Sigma)
 - assemble_augmented_rhs   uno/ingredients/subproblem/Subproblem.cpp:80-99
 - assemble_direction       uno/ingredients/inequality_handling_methods/interior_point_methods/
                            PrimalDualInteriorPointProblem.cpp:173-194 (assemble_primal_dual_direction),
                            :262-278 (compute_bound_dual_direction), :281-325 (fraction-to-boundary)
 - symv / quadratic_product uno/linear_algebra/SymmetricMatrix.hpp:100-130 (COO order)
 
+Pinned to the reference itself: tests/golden/ipm_reference_vectors.json holds the outputs of those very
+reference functions (compiled from /root/reference, tests/golden/make_ipm_fixtures.sh) on seeded inputs, and
+tests/test_ipm_vectors.py requires this restatement to reproduce them bit for bit.
+
 Only tests/ may import this module; the product path is uno_amd/csrc/ipm_kernels.hip.
 """
 import numpy as np
+
+
+def barrier_diagonal(x, lb, ub, zl, zu):
+    """(variables, Sigma): for every variable with a finite bound, ascending, 0 + zl/(x - lb) [finite lb]
+    + zu/(x - ub) [finite ub] (PrimalDualInteriorPointProblem.cpp:62-77, the order Uno inserts them)."""
+    var, sig = [], []
+    for i in range(len(x)):
+        fl, fu = np.isfinite(lb[i]), np.isfinite(ub[i])
+        if fl or fu:
+            d = 0.0
+            if fl:
+                d += zl[i] / (x[i] - lb[i])
+            if fu:
+                d += zu[i] / (x[i] - ub[i])
+            var.append(i)
+            sig.append(d)
+    return np.array(var, dtype=np.int64), np.array(sig)
 
 
 def assemble_augmented_rhs(grad, cons, y, jac_con, jac_var, jac_val):

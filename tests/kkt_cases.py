@@ -43,3 +43,29 @@ def null_threshold_case(N, ks, block_scale=1.0, sweeps=3):
     nnull = sum(1 for k in ks if k * EPS <= EPS * kstar)
     inertia = (N + len(ks), 1 + len(ks) - nnull, nnull)
     return n, np.array(rows, np.int64), np.array(cols, np.int64), np.array(vals), inertia, kstar
+
+
+def delay_case(N, eps_exp, d_hub=3.0, seed=0):
+    """Fronts whose ONLY admissible pivots fail the threshold u = 0.01 (MUMPS CNTL(1), sym = 2): a hub (dense
+    row: ordered last by both orderings, so it is never fully summed in a leaf front) joined with entries 1 to
+    N spokes whose diagonals are +-10^e (e in eps_exp, cycled; signs random).  A leaf front's fully-summed
+    block is then diagonal with |a_ii| = 10^e < u * 1 and has no off-diagonal for a 2x2 pivot, so MUMPS delays
+    every column to the parent (the oracle does); delay_relaxed = 0 instead accepts them at a relaxed
+    threshold (growth up to 10^-e).  Every spoke row has maximum 1 (its hub entry), so the equilibration
+    leaves |a_ii| = 10^e below u; the inertia is analytic: Sylvester on [[D, e], [e^T, d]] gives inertia(D)
+    plus the sign of the Schur complement d - sum 1/d_i, kept away from 0 (N must exceed 10 sqrt(N + 1),
+    the dense-row cut of the analysis)."""
+    rng = np.random.default_rng(seed)
+    e = np.array([eps_exp[i % len(eps_exp)] for i in range(N)], dtype=float)
+    d = rng.choice([-1.0, 1.0], N) * 10.0 ** e
+    schur = d_hub - np.sum(1.0 / d)
+    if abs(schur) < 1.0:  # keep the decision away from rounding
+        d_hub += 10.0 * np.sign(schur if schur != 0 else 1.0)
+        schur = d_hub - np.sum(1.0 / d)
+    n = N + 1
+    rows = [N] + list(range(N)) + [N] * N
+    cols = [N] + list(range(N)) + list(range(N))
+    vals = [d_hub] + list(d) + [1.0] * N
+    pos = int((d > 0).sum()) + (1 if schur > 0 else 0)
+    inertia = (pos, n - pos, 0)
+    return n, np.array(rows, np.int64), np.array(cols, np.int64), np.array(vals), inertia

@@ -57,3 +57,49 @@ def test_gpu_threshold_matches_oracle(block_scale, overlap_norm):
             keep[1 + N_HUB + 2 * t: 3 + N_HUB + 2 * t] = False
     np.testing.assert_allclose(xg[keep], xo[keep], rtol=1e-10, atol=1e-12)
     assert np.isfinite(xg).all()
+
+
+def test_oracle_delays_on_failing_fronts():
+    """CPU: the oracle (MUMPS semantics) delays the failing spoke columns and reports the analytic inertia."""
+    from kkt_cases import delay_case
+    for exps in ([-3], [-5, -7], [-9, -4, -6]):
+        n, r, c, v, inertia = delay_case(300, exps)
+        o = OracleKKT()
+        o.analyze(n, r, c)
+        o.factorize(v)
+        assert o.inertia() == inertia, exps
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exps", [[-3], [-5, -7], [-9, -4, -6]])
+def test_relaxed_vs_delayed_pivots(exps):
+    """a front whose only admissible pivots fail u.  MUMPS (and the oracle) delay the columns to
+    the parent; the shipped plugin mode (delay_relaxed = 0, integration/HIPLDLSolver.cpp) accepts them at a
+    relaxed threshold and refines the solve.  Both modes must give the oracle's (= the analytic) inertia,
+    and both solutions must meet the residual bar; the scenario itself is asserted (relaxed pivots in one
+    mode, merged fronts in the other)."""
+    import uno_amd
+    from kkt_cases import delay_case
+    from test_gpu_parity import rel_residual
+    uno_amd.load_library()
+    n, r, c, v, inertia = delay_case(300, exps)
+    o = OracleKKT()
+    o.analyze(n, r, c)
+    o.factorize(v)
+    assert o.inertia() == inertia
+    b = np.sin(np.arange(n, dtype=np.float64) + 0.5)
+    xo = o.solve(b)
+    for relaxed in (0, 1):
+        g = uno_amd.HipKKT(0, delay_relaxed=relaxed)
+        g.analyze(n, r, c)
+        g.factorize(v)
+        assert g.inertia() == inertia, (relaxed, g.inertia())
+        st = g.stats()
+        if relaxed == 0:
+            assert st["pivots_relaxed"] > 0 and st["fronts_merged"] == 0
+        else:
+            assert st["fronts_merged"] > 0
+        x = g.solve(b)
+        assert rel_residual(n, r, c, v, x, b) < 1e-10, relaxed
+        np.testing.assert_allclose(x, xo, rtol=1e-8, atol=1e-10 * np.abs(xo).max())
+        g.close()

@@ -174,14 +174,18 @@ def run_model(model, solver):
 
 
 def same_large_run(r, g, rel=1e-10):
+    """north_star's bar on the large synthetic runs: identical iterate sequence (iterations, factorization /
+    solve counts, every factorization's inertia), and objective, primal summaries (sum, sum of squares, max
+    |x|), every multiplier summary and the reference's own primal / dual residual measures of the final
+    iterate (Iterate.hpp:43-46) within `rel` = 1e-10 relative to max(1, |golden|)."""
     assert r["status"] == g["status"] == 0
     assert r["iterations"] == g["iterations"]
     assert r["factorizations"] == g["factorizations"] and r["solves"] == g["solves"]
     assert r["inertia_trace"] == g["inertia_trace"]
-    assert abs(r["objective"] - g["objective"]) <= rel * abs(g["objective"])
+    assert abs(r["objective"] - g["objective"]) <= rel * max(1.0, abs(g["objective"]))
     for a, b in zip(r["primals_summary"], g["primals_summary"]):
-        assert abs(a - b) <= 1e-8 * max(1.0, abs(b))
-    same_duals(r, g, 1e-8)
+        assert abs(a - b) <= rel * max(1.0, abs(b)), ("primals_summary", a, b)
+    same_duals(r, g, rel)
 
 
 @needs_driver
