@@ -226,6 +226,23 @@ def test_hipldl_plugin_arrowband_1e5():
     same_large_run(run_model("arrowband:100000", "HIPLDL"), g)
 
 
+C3_GOLDEN = os.path.join(ROOT, "tests", "golden", "arrowband1000000_uno_oracle.json")
+
+
+@needs_driver
+@pytest.mark.gpu
+@pytest.mark.timeout(850)
+def test_hipldl_plugin_arrowband_1e6():
+    """north_star at the headline size, configs[2]: KKT dimension 1e6, nnz 2e7 (golden: the ORACLE run of
+    tests/golden/make_c3_golden.sh, container CPU time).  The GPU plugin inside the reference Uno core must
+    give the identical iterate sequence -- iterations, factorization and solve counts, every factorization's
+    inertia -- and objective, primal summaries, every multiplier summary and the final residual measures
+    within 1e-10 relative."""
+    g = json.load(open(C3_GOLDEN))
+    assert g["status"] == 0 and g["iterations"] > 100
+    same_large_run(drive(["arrowband:1000000", "linear_solver=HIPLDL"], 800), g)
+
+
 @needs_driver
 @pytest.mark.gpu
 def test_hipldl_plugin_arrowband_inequalities_1e5():
