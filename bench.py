@@ -43,9 +43,13 @@ def parse():
     ap.add_argument("--n", type=int, default=0,
                     help="KKT dimension per GPU (default: 1e6 = C3 on one GPU / in replicas; 5e5 per GPU in dist mode, "
                          "C5 = 4e6 at 8 GPUs)")
-    ap.add_argument("--mode", choices=["dist", "replicas", "ipm"], default="dist",
-                    help="N>1: one system partitioned over the GPUs (dist) or one system per GPU (replicas); "
-                         "ipm: an interior-point-like sequence through the drop-in's host-value path (1 GPU)")
+    ap.add_argument("--mode", choices=["dist", "replicas", "ipm"], default=None,
+                    help="default: dist for N>1, the C3 system for N=1.  dist: one C5-family system of N x 5e5 rows "
+                         "partitioned over the GPUs (also at N=1: the same-size N=1 point of the scaling curve); "
+                         "replicas: one C3 system per GPU; ipm: an interior-point-like sequence through the "
+                         "drop-in's host-value path (1 GPU)")
+    ap.add_argument("--no-shipped", action="store_true",
+                    help="skip the second line measured in the Uno plugin's configuration (delay_relaxed=0 + refinement)")
     ap.add_argument("--ipm-iters", type=int, default=12)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-n", type=int, default=1_000_000)
@@ -186,7 +190,7 @@ def main():
             seed, n_total = uno_amd.SEEDS["C3"] + rank, args.n or 1_000_000
         n, nv, m, rows, cols, vals, rhs = uno_amd.arrowband(n_total, seed)
         kkt = uno_amd.HipKKT(local)
-        if dist_mode:
+        if dist_mode and world > 1:
             from uno_amd.replicas import share_bytes
             uid = share_bytes(uno_amd.rccl_unique_id() if rank == 0 else None, world)
             kkt.attach_rccl(uid, rank, world)
@@ -204,7 +208,8 @@ def main():
         torch.cuda.synchronize()
         return n_total, (n, nv, m, rows, cols, vals, rhs), kkt, t_analysis, vals_d, rhs_d, x_d
 
-    dist_mode = world > 1 and args.mode == "dist"
+    mode = args.mode or ("dist" if world > 1 else "single")
+    dist_mode = mode == "dist"
     dist_fallback = None
     if dist_mode:
         # the partitioned path is checked once before timing; a rank that fails (RCCL or device error)
@@ -226,6 +231,22 @@ def main():
     if not dist_mode:
         n_total, gen, kkt, t_analysis, vals_d, rhs_d, x_d = build(False)
     n, nv, m, rows, cols, vals, rhs = gen
+
+    def first_factorization():
+        """The first factorization of a pattern, timed alone: with MUMPS-style delays it includes the merge
+        rounds (a delayed column moves into the parent front: host structure rebuild + refactorization)."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        kkt_ = kkt
+        kkt_.factorize(device_ptr=vals_d.data_ptr())
+        kkt_.inertia()
+        torch.cuda.synchronize()
+        return 1e3 * (time.perf_counter() - t1)
+
+    first_ms = first_factorization()
+    first_merges = kkt.stats()["fronts_merged"]
 
     def step():
         kkt.factorize(device_ptr=vals_d.data_ptr())
@@ -261,7 +282,8 @@ def main():
         absk = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max()
         rel_res = float(res / (absk * np.abs(x).max() + np.abs(rhs).max()))
     st = kkt.stats()
-    dinfo = kkt.dist_info() if dist_mode else None
+    dinfo = kkt.dist_info() if dist_mode and world > 1 else None
+    assert st["solve_aborts"] == 0, f"dataflow solve aborted {st['solve_aborts']} times (level-scheduled redo)"
 
     # second timed pass with per-kernel HIP events on the solver stream (roofline)
     ktimes = {}
@@ -273,6 +295,42 @@ def main():
         torch.cuda.synchronize()
         ktimes = kkt.kernel_times()
         kkt.set_option("timing", 0)
+
+    # ---- the same step in the Uno plugin's configuration (integration/HIPLDLSolver.cpp:15-27): threshold
+    # relaxation instead of delayed pivots (delay_relaxed=0) and one refinement step per solve after a
+    # factorization that relaxed a pivot.  Single-GPU lines only (the plugin drives one GPU).
+    shipped = None
+    if world == 1 and not args.no_shipped and not args.profile_only:
+        ks = uno_amd.HipKKT(local, delay_relaxed=0)
+        ks.set_option("dataflow_solve", args.dataflow)
+        ks.analyze(n, rows, cols)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        ks.factorize(device_ptr=vals_d.data_ptr())
+        s_inertia = ks.inertia()
+        torch.cuda.synchronize()
+        s_first = 1e3 * (time.perf_counter() - t1)
+        xs_d = torch.empty_like(rhs_d)
+
+        def sstep():
+            ks.factorize(device_ptr=vals_d.data_ptr())
+            i_ = ks.inertia()
+            ks.solve_device(rhs_d.data_ptr(), xs_d.data_ptr())
+            return i_
+        s_elapsed, s_inertia = timed_steps(sstep, args.steps, args.warmup, torch.cuda.synchronize, 1, dev)
+        sst = ks.stats()
+        xsv = xs_d.cpu().numpy()
+        sres = np.abs(uno_amd.coo_symv(n, rows, cols, vals, xsv) - rhs).max()
+        sabs = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max()
+        shipped = {"value": round(args.steps / s_elapsed, 4), "unit": "factor+solve/s",
+                   "ms_per_step": round(1e3 * s_elapsed / args.steps, 4),
+                   "first_factorization_ms": round(s_first, 3),
+                   "options": "delay_relaxed=0, refine=1 (HIPLDLSolver.cpp)",
+                   "pivots_relaxed": sst["pivots_relaxed"], "fronts_merged": sst["fronts_merged"],
+                   "refinement_steps_per_solve": 1 if sst["pivots_relaxed"] > 0 else 0,
+                   "inertia": list(s_inertia), "inertia_equal_to_headline": tuple(s_inertia) == tuple(inertia),
+                   "rel_residual": float(sres / (sabs * np.abs(xsv).max() + np.abs(rhs).max()))}
+        del ks
 
     if rank != 0:
         if world > 1:
@@ -290,7 +348,7 @@ def main():
     n2 = st["pivots_2x2"]
     bytes_solve = 8.0 * (2 * st["nnz_L"] + n + n2) + 24.0 * n      # SURVEY 8(d) B_solve, per solve
     flops_fac = st["flops"]                                         # per factorization
-    if dist_mode:  # rank 0's share: its subtrees + the top of the tree
+    if dinfo:  # rank 0's share: its subtrees + the top of the tree
         flops_fac = dinfo["my_flops"] + dinfo["top_flops"]
     bytes_fac = 8.0 * (st["nnz_unique"] + st["nnz_L"] + n)          # B_min per factorization
     roof = None
@@ -378,12 +436,19 @@ def main():
             model = [l.split(":", 1)[1].strip() for l in open("/proc/cpuinfo") if l.startswith("model name")][0]
         except Exception:  # noqa: BLE001 -- informational
             pass
+        try:
+            affinity = len(os.sched_getaffinity(0))
+        except Exception:  # noqa: BLE001 -- informational
+            affinity = None
         cpu = {"value": round(1.0 / float(np.median(per)), 4), "unit": "factor+solve/s", "cores": threads(),
                "kind": "port",
                "sample": f"oracle/cpu_mf.cpp (multi-threaded multifrontal restatement on the product's ND analysis; "
                          f"MUMPS unavailable) on arrowband n={cn} nnz={len(cv)}: median of {reps} "
                          f"factor+inertia+solve reps ({t_cpu:.1f} s), {threads()} OpenMP threads",
-               "nproc": os.cpu_count(), "cpu_model": model,
+               "nproc": os.cpu_count(), "affinity_cpus": affinity,
+               "cores_note": "OpenMP threads = OMP_NUM_THREADS, the CPU share the GPU lease grants per GPU "
+                             "(16 on the box; nproc / affinity show the whole host)",
+               "cpu_model": model,
                "inertia": list(o_inertia), "inertia_checked_against_gpu": cn == n,
                "gpu_over_cpu": round(value / (1.0 / float(np.median(per))), 1) if per else None}
 
@@ -411,12 +476,18 @@ def main():
                    "pivots_2x2": st["pivots_2x2"], "pivots_relaxed": st["pivots_relaxed"],
                    "solve_schedule": f"dataflow grid {st['solve_grid']}" if st["solve_grid"] else "level-synchronous",
                    "fronts_merged": st["fronts_merged"], "rel_residual": rel_res,
+                   "first_factorization_ms": round(first_ms, 3),
+                   "first_factorization_note": "timed alone after the warm-up-free analysis: MUMPS-style delays "
+                                               "(delay_relaxed=1) are resolved here by merge rounds "
+                                               f"({first_merges} fronts merged); the timed steps refactor the merged structure",
+                   "solve_aborts": st["solve_aborts"],
                    "parallelism": (f"subtree-partitioned x{world} (RCCL root exchange to rank 0)" if dist_mode
                                    else f"replicas x{world} (independent KKT per GPU)"),
                    "value_unit_note": "n=1e6-equivalent factor+solves per second of the whole job",
                    "dist": dinfo, "dist_fallback": dist_fallback},
         "roofline": roof,
         "cpu_baseline": cpu,
+        "shipped_plugin_mode": shipped,
     }
     print(json.dumps(out))
     if world > 1:

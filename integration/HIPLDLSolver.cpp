@@ -118,6 +118,11 @@ namespace uno {
       this->values_fresh = false;
       this->check(this->backend.inertia(this->handle, &this->positive, &this->negative, &this->zero), "inertia");
       kkt_trace::record_factorization(this->dimension, this->positive, this->negative, this->zero);
+      const size_t index = kkt_trace::factor_count()++;
+      if (kkt_trace::factor_hook() != nullptr) {
+         kkt_trace::factor_hook()(index, this->dimension, static_cast<int64_t>(this->row_indices.size()), this->row_indices.data(),
+            this->column_indices.data(), matrix.data_pointer(), this->positive, this->negative, this->zero);
+      }
    }
 
    // MUMPSSolver.cpp:91-96 (JOB=3): the matrix argument is ignored, the last factorization is used

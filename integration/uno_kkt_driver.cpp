@@ -8,12 +8,17 @@
 //        uno_kkt_driver convexify:<model> [option=value ...]   byrd-preset Hessian convexification only (see below)
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <algorithm>
+#include <sstream>
+#include <vector>
 #include <iostream>
 #include <memory>
 #include <string>
 
 #include "KKTTrace.hpp"
+#include "kkt_oracle.h"
+#include "uno_kkt.h"
 #include "Uno.hpp"
 #include "model/ModelFactory.hpp"
 #include "models/HS015Model.hpp"
@@ -36,6 +41,93 @@
 #include "tools/UserCallbacks.hpp"
 
 using namespace uno;
+
+// ---- inertia cross-check (UNO_KKT_CROSSCHECK="i,j,..."): at the listed factorizations of the run, the matrix
+// the plugin factored is factored again by the CPU oracle and (where a GPU exists) by a fresh GPU handle, and
+// also shifted by -+sigma on its diagonal for a ladder of sigma relative to ||A||_inf.  Where two solvers report
+// different inertias for nearly the same matrix, the ladder shows whether an eigenvalue lies within sigma of 0
+// (its sign is then decided by rounding, not by the matrix).  Test drivers only.
+namespace {
+   std::vector<size_t> crosscheck_targets;
+   std::vector<std::string> crosscheck_records;
+
+   std::string inertia_json(int rc, int64_t p, int64_t q, int64_t z) {
+      if (rc != 0) return "null";
+      std::ostringstream o;
+      o << "[" << p << ", " << q << ", " << z << "]";
+      return o.str();
+   }
+
+   void crosscheck_hook(size_t index, size_t n, int64_t nnz, const int64_t* r, const int64_t* c, const double* v,
+         int64_t p, int64_t q, int64_t z) {
+      if (std::find(crosscheck_targets.begin(), crosscheck_targets.end(), index) == crosscheck_targets.end()) return;
+      std::vector<double> rowsum(n, 0.);
+      std::vector<int64_t> diag(n, -1);
+      for (int64_t e = 0; e < nnz; ++e) {
+         rowsum[r[e]] += std::fabs(v[e]);
+         if (r[e] != c[e]) rowsum[c[e]] += std::fabs(v[e]);
+         else if (diag[r[e]] < 0) diag[r[e]] = e;
+      }
+      double anorm = 0.;
+      for (double x: rowsum) anorm = std::max(anorm, x);
+      bool all_diag = true;
+      for (int64_t d: diag) all_diag = all_diag && d >= 0;
+      oracle_kkt_t o = oracle_kkt_create();
+      uno_kkt_t g = nullptr;
+      const bool gpu = uno_kkt_create(&g, 0) == UNO_KKT_OK;
+      int orc = oracle_kkt_analyze(o, (int64_t)n, nnz, r, c);
+      int grc = gpu ? uno_kkt_analyze(g, (int64_t)n, nnz, r, c) : -1;
+      auto factor_both = [&](const double* w, std::string& jo, std::string& jg) {
+         int64_t a = 0, b = 0, d = 0;
+         int rc = orc == 0 ? oracle_kkt_factorize(o, w) : orc;
+         if (rc == 0) rc = oracle_kkt_inertia(o, &a, &b, &d);
+         jo = inertia_json(rc, a, b, d);
+         if (gpu && grc == 0) {
+            rc = uno_kkt_factorize(g, w, 0);
+            if (rc == UNO_KKT_OK || rc == UNO_KKT_ERR_PIVOT) rc = uno_kkt_inertia(g, &a, &b, &d);
+            jg = inertia_json(rc, a, b, d);
+         } else {
+            jg = "null";
+         }
+      };
+      std::ostringstream out;
+      std::string jo, jg;
+      factor_both(v, jo, jg);
+      out.precision(17);
+      out << "{\"index\": " << index << ", \"run_inertia\": " << inertia_json(0, p, q, z) << ", \"oracle\": " << jo
+          << ", \"gpu\": " << jg << ", \"anorm_inf\": " << anorm << ", \"shifts\": [";
+      if (all_diag) {
+         std::vector<double> w(v, v + nnz);
+         const double rel[] = {1e-6, 1e-8, 1e-10, 1e-12, 1e-14};
+         for (size_t k = 0; k < sizeof(rel) / sizeof(rel[0]); ++k) {
+            const double sigma = rel[k] * anorm;
+            std::string op, gp, om, gm;
+            for (size_t i = 0; i < n; ++i) w[diag[i]] = v[diag[i]] + sigma;
+            factor_both(w.data(), op, gp);
+            for (size_t i = 0; i < n; ++i) w[diag[i]] = v[diag[i]] - sigma;
+            factor_both(w.data(), om, gm);
+            out << (k ? ", " : "") << "{\"sigma_rel\": " << rel[k] << ", \"oracle_plus\": " << op << ", \"oracle_minus\": " << om
+                << ", \"gpu_plus\": " << gp << ", \"gpu_minus\": " << gm << "}";
+         }
+      }
+      out << "]}";
+      crosscheck_records.push_back(out.str());
+      std::fprintf(stderr, "[crosscheck] %s\n", crosscheck_records.back().c_str());
+      oracle_kkt_destroy(o);
+      if (gpu) uno_kkt_destroy(g);
+   }
+
+   void install_crosscheck() {
+      const char* env = std::getenv("UNO_KKT_CROSSCHECK");
+      if (env == nullptr) return;
+      std::stringstream ss(env);
+      std::string item;
+      while (std::getline(ss, item, ',')) {
+         if (!item.empty()) crosscheck_targets.push_back(std::stoul(item));
+      }
+      kkt_trace::factor_hook() = crosscheck_hook;
+   }
+} // namespace
 
 // The byrd preset's use of the plugin: Hessian convexification by
 // PrimalRegularization::regularize_hessian (PrimalRegularization.hpp:79-129) of the l1-relaxed problem's
@@ -100,6 +192,7 @@ int main(int argc, char* argv[]) {
       return 2;
    }
    std::string model_name = argv[1];
+   install_crosscheck();
    const bool convexify = model_name.rfind("convexify:", 0) == 0;
    if (convexify) model_name = model_name.substr(10);
    try {
@@ -187,6 +280,8 @@ int main(int argc, char* argv[]) {
             static_cast<long long>(e.negative), static_cast<long long>(e.zero));
          first = false;
       }
+      std::printf("], \"crosscheck\": [");
+      for (size_t k = 0; k < crosscheck_records.size(); ++k) std::printf("%s%s", k ? ", " : "", crosscheck_records[k].c_str());
       std::printf("]}\n");
    }
    catch (std::exception& exception) {
