@@ -57,6 +57,7 @@ def parse():
     ap.add_argument("--leaf", type=int, default=0, help="nested-dissection leaf size (0 = library default)")
     ap.add_argument("--block", type=int, default=0, help="max supernode width (0 = library default)")
     ap.add_argument("--dataflow", type=int, default=1, help="1: one-launch dataflow solve, 0: level-scheduled solve")
+    ap.add_argument("--opt", action="append", default=[], help="library option name=value (A/B experiments)")
     return ap.parse_args()
 
 
@@ -199,6 +200,9 @@ def main():
         if args.block:
             kkt.set_option("max_block", args.block)
         kkt.set_option("dataflow_solve", args.dataflow)
+        for kv in args.opt:
+            k_, v_ = kv.split("=", 1)
+            kkt.set_option(k_, float(v_))
         t0 = time.perf_counter()
         kkt.analyze(n, rows, cols)
         t_analysis = time.perf_counter() - t0

@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include <array>
+#include <fstream>
 #include <sstream>
 #include <vector>
 #include <iostream>
@@ -50,6 +52,11 @@ using namespace uno;
 namespace {
    std::vector<size_t> crosscheck_targets;
    std::vector<std::string> crosscheck_records;
+   // UNO_KKT_CROSSCHECK_TRACE=<file of "p q z" lines, a golden run's inertias>: cross-check where this run first
+   // reports another inertia than the golden one, and where it first disagrees on whether the inertia is the
+   // expected one (the golden run's last factorization), i.e. where the two runs' decisions part
+   std::vector<std::array<int64_t, 3>> crosscheck_golden;
+   bool crosscheck_first_done = false, crosscheck_decision_done = false;
 
    std::string inertia_json(int rc, int64_t p, int64_t q, int64_t z) {
       if (rc != 0) return "null";
@@ -60,7 +67,17 @@ namespace {
 
    void crosscheck_hook(size_t index, size_t n, int64_t nnz, const int64_t* r, const int64_t* c, const double* v,
          int64_t p, int64_t q, int64_t z) {
-      if (std::find(crosscheck_targets.begin(), crosscheck_targets.end(), index) == crosscheck_targets.end()) return;
+      std::string tag = "listed";
+      if (std::find(crosscheck_targets.begin(), crosscheck_targets.end(), index) == crosscheck_targets.end()) {
+         if (index >= crosscheck_golden.size() || crosscheck_golden.empty()) return;
+         const auto& g = crosscheck_golden[index];
+         const auto& e = crosscheck_golden.back();
+         const bool differs = g[0] != p || g[1] != q || g[2] != z;
+         const bool decision = (g == e) != (p == e[0] && q == e[1] && z == e[2]);
+         if (differs && !crosscheck_first_done) { crosscheck_first_done = true; tag = decision ? "first_difference+first_decision" : "first_difference"; if (decision) crosscheck_decision_done = true; }
+         else if (decision && !crosscheck_decision_done) { crosscheck_decision_done = true; tag = "first_decision"; }
+         else return;
+      }
       std::vector<double> rowsum(n, 0.);
       std::vector<int64_t> diag(n, -1);
       for (int64_t e = 0; e < nnz; ++e) {
@@ -94,7 +111,9 @@ namespace {
       std::string jo, jg;
       factor_both(v, jo, jg);
       out.precision(17);
-      out << "{\"index\": " << index << ", \"run_inertia\": " << inertia_json(0, p, q, z) << ", \"oracle\": " << jo
+      out << "{\"index\": " << index << ", \"tag\": \"" << tag << "\"";
+      if (index < crosscheck_golden.size()) out << ", \"golden_inertia\": " << inertia_json(0, crosscheck_golden[index][0], crosscheck_golden[index][1], crosscheck_golden[index][2]);
+      out << ", \"run_inertia\": " << inertia_json(0, p, q, z) << ", \"oracle\": " << jo
           << ", \"gpu\": " << jg << ", \"anorm_inf\": " << anorm << ", \"shifts\": [";
       if (all_diag) {
          std::vector<double> w(v, v + nnz);
@@ -118,6 +137,12 @@ namespace {
    }
 
    void install_crosscheck() {
+      if (const char* path = std::getenv("UNO_KKT_CROSSCHECK_TRACE")) {
+         std::ifstream in(path);
+         int64_t a, b, c;
+         while (in >> a >> b >> c) crosscheck_golden.push_back({a, b, c});
+         kkt_trace::factor_hook() = crosscheck_hook;
+      }
       const char* env = std::getenv("UNO_KKT_CROSSCHECK");
       if (env == nullptr) return;
       std::stringstream ss(env);

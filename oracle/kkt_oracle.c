@@ -31,6 +31,7 @@ struct oracle_kkt {
     int analyzed, factored;
     double u;
     int scale_iters;
+    int ordering;  /* 0: reverse Cuthill-McKee (default), 1: Cuthill-McKee (not reversed) -- a second valid ordering */
     double null_fac;
     char err[256];
     /* canonical pattern */
@@ -110,6 +111,7 @@ void oracle_kkt_destroy(oracle_kkt_t h) {
 int oracle_kkt_set_option(oracle_kkt_t h, const char* name, double value) {
     if (!strcmp(name, "pivot_threshold")) { h->u = value; return 0; }
     if (!strcmp(name, "scale_iters")) { h->scale_iters = (int)value; return 0; }
+    if (!strcmp(name, "ordering")) { h->ordering = (int)value; return 0; }
     if (!strcmp(name, "null_tol_factor")) { h->null_fac = value; return 0; }
     return fail(h, "unknown option '%s'", name);
 }
@@ -261,7 +263,7 @@ int oracle_kkt_analyze(oracle_kkt_t h, int64_t n, int64_t nnz, const int64_t* ro
     /* reverse the Cuthill-McKee order, then dense nodes */
     h->perm = (int64_t*)xcalloc((size_t)n + 1, sizeof(int64_t));
     h->iperm = (int64_t*)xcalloc((size_t)n + 1, sizeof(int64_t));
-    for (int64_t q = 0; q < norder; ++q) h->perm[q] = order[norder - 1 - q];
+    for (int64_t q = 0; q < norder; ++q) h->perm[q] = h->ordering == 1 ? order[q] : order[norder - 1 - q];
     int64_t nq = norder;
     for (int64_t i = 0; i < n; ++i) if (dense[i]) h->perm[nq++] = i;
     for (int64_t q = 0; q < n; ++q) h->iperm[h->perm[q]] = q;

@@ -1,13 +1,20 @@
 // OracleBackend.cpp -- TEST INFRASTRUCTURE ONLY: the CPU oracle (oracle/kkt_oracle.c) behind the same
 // Uno plugin adapter as the GPU backend, registered as linear_solver=ORACLE in test builds.  Used to
 // produce golden Uno traces (tests/golden/) that the GPU run must reproduce.
+#include <cstdlib>
 #include <memory>
 #include "HIPLDLSolver.hpp"
 #include "kkt_oracle.h"
 
 namespace uno {
    namespace {
-      void* o_create() { return oracle_kkt_create(); }
+      // UNO_ORACLE_ORDERING=1: Cuthill-McKee instead of its reverse (a second valid ordering, to show how far
+      // a whole solve's trace depends on the rounding of one ordering; tests/golden/make_c3_golden.sh)
+      void* o_create() {
+         oracle_kkt_t h = oracle_kkt_create();
+         if (const char* o = std::getenv("UNO_ORACLE_ORDERING")) oracle_kkt_set_option(h, "ordering", std::atof(o));
+         return h;
+      }
       void o_destroy(void* h) { oracle_kkt_destroy(static_cast<oracle_kkt_t>(h)); }
       int o_analyze(void* h, int64_t n, int64_t nnz, const int64_t* r, const int64_t* c) {
          return oracle_kkt_analyze(static_cast<oracle_kkt_t>(h), n, nnz, r, c);

@@ -204,6 +204,11 @@ struct uno_kkt {
     // dataflow factorization of the upper tree (levels >= dff_level, every front one-wave); option
     // "dataflow_factor" (default 1)
     int concurrent_classes = 1;  // option "concurrent_classes"
+    int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
+                                 // factorization (1), also before every sweep (2)
+    int sweep_coalesced = 1;     // option "sweep_coalesced"
+    DBuf<double> fscale;
+    DBuf<int8_t> flong;          // per front row: index of its row among the long rows, -1 otherwise
     int dff_enabled = 1;  // 0 off, 1 (default) levels >= L*, 2 also the small fronts below them (measured no faster at C3)
     int dff_level = INT32_MAX;     // first level of the dataflow launch (INT32_MAX: none)
     int dff_mmax = 0;
@@ -1094,6 +1099,11 @@ int upload_structure(uno_kkt_t h) {
             if (lr.size() > 127) h->use_front_sweeps = false;  // int8 index
             HIPCHK(h, h->longpos.upload(lp, s));
             HIPCHK(h, h->long_orig.upload(lo, s));
+            {  // the same per front row (the sweeps read it with the row ids, no dependent gather)
+                std::vector<int8_t> fl(std::max<size_t>(S.rows.size(), 1), (int8_t)-1);
+                for (size_t t = 0; t < S.rows.size(); ++t) fl[t] = lp[S.rows[t]];
+                HIPCHK(h, h->flong.upload(fl, s));
+            }
             const int64_t npl = std::max<int64_t>((int64_t)S.nf * (int64_t)lr.size(), 1);
             HIPCHK(h, h->part_long.alloc(npl));
             // fronts without a given long row never write its partial: those slots stay 0
@@ -1127,6 +1137,7 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->big.alloc(S.max_m > kMaxLdsFront ? S.nf : 0));
     if (!h->big_pending.p) HIPCHK(h, h->big_pending.alloc(1));
     HIPCHK(h, h->frow.alloc(S.rows.size()));
+    HIPCHK(h, h->fscale.alloc(S.rows.size()));
     HIPCHK(h, h->fpos.alloc(S.rows.size()));
     HIPCHK(h, h->piv.alloc(S.rows.size()));
     if (!h->counters.p) {
@@ -1208,6 +1219,10 @@ int enqueue_factorization(uno_kkt_t h) {
             W.rmax = reinterpret_cast<unsigned long long*>(h->rmax.p); W.longpos = h->longpos.p;
             W.long_orig = h->long_orig.p; W.n_long = h->n_long; W.part_long = h->part_long.p; W.max_m = (int)S.max_m;
             W.big_list = h->sweep_big.p; W.n_big = h->n_sweep_big; W.big_slices = h->sweep_slices;
+            W.fscale = h->front_scale == 2 ? h->fscale.p : nullptr;  // measured slower: 3 extra gathers (r03)
+            W.coalesced = h->sweep_coalesced;
+            W.rows_total = (int64_t)S.rows.size();
+            W.flong = h->n_long > 0 ? h->flong.p : nullptr;
             HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
             if (h->overlap_norm && !h->exact_next) {
                 h->last_optimistic = true;  // row sums only if a pivot is small (sync_and_verify)
@@ -1231,7 +1246,11 @@ int enqueue_factorization(uno_kkt_t h) {
             if (rc != UNO_KKT_OK) return rc;
         }
     }
+    // the scaling per front row (the front sweeps leave it gathered after their last update)
+    if (h->front_scale && !(h->use_front_sweeps && h->scale_iters > 0 && h->front_scale == 2))
+        HIPCHK(h, launch_front_scale(h->rows.p, h->scale.p, h->fscale.p, (int64_t)S.rows.size(), s));
     FactorArgs A;
+    A.fscale = h->front_scale ? h->fscale.p : nullptr;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
     A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
@@ -1427,6 +1446,8 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
+    else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
+    else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;
     else if (n == "dist_force") h->dist_force = value != 0.0;

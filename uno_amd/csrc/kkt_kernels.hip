@@ -468,28 +468,78 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
         e0 += chunk * blockIdx.y;
         e1 = e0 + chunk < e1 ? e0 + chunk : e1;
     }
-    // Each lane takes EB consecutive slots: slots are ordered by (column, row), so a lane's slots mostly
-    // share a column and the column maximum is kept in a register, flushed to LDS when the column
-    // changes (one LDS atomic per run instead of one per slot on a single, conflicting address).
+    // A batch is EB x NT consecutive slots.  Coalesced (default): load u of lane l reads slot base + u NT + l,
+    // so a wave's load instruction covers 256 / 512 contiguous bytes, and every slot does one LDS atomic max
+    // for its row and one for its column.  Otherwise (option sweep_coalesced = 0) each lane takes EB
+    // consecutive slots, keeping its column maximum in a register (one LDS atomic per column run), but each
+    // load instruction then spans NT strided cache lines: 8x the address-unit requests per slot.
     constexpr int EB = 8;
+    const bool coal = A.coalesced != 0;
     uint32_t lp[EB];
     double v[EB];
-    auto load = [&](int64_t eb) {
+    auto load = [&](int64_t base) {
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-            const int64_t e = eb + u;
+            const int64_t e = coal ? base + (int64_t)u * NT + lane : base + (int64_t)lane * EB + u;
             const bool ok = e < e1;
             lp[u] = ok ? A.ent_lpos[e] : 0xffffffffu;
             v[u] = ok ? A.uval[e] : 0.0;
         }
     };
-    load(e0 + (int64_t)lane * EB);  // the first batch is in flight while the rows' scalings are gathered
-    for (int q = lane; q < m; q += NT) {
-        rm[q] = 0ull;
-        if (!FIRST) sl[q] = A.scale[A.rows[ro + q]];
+    load(e0);  // the first batch is in flight while the rows' scalings are gathered
+    // one-wave fronts of <= 128 rows keep their row ids and long-row indices in registers for the final
+    // flush, and read the rows' scalings from the per-front-row copy (fscale, gathered after the previous
+    // sweep's update): every load of the front is issued in the first round trip (no rows -> scale or
+    // rows -> longpos chain)
+    constexpr int RQ = 2;
+    const bool regrows = !BIG && m <= 64 * RQ;
+    int32_t rr[RQ];
+    int lk[RQ];
+    if (regrows) {
+        double sv[RQ];
+#pragma unroll
+        for (int u = 0; u < RQ; ++u) {
+            const int q = lane + 64 * u;
+            const bool ok = q < m;
+            rr[u] = ok ? A.rows[ro + q] : 0;
+            lk[u] = ok && A.flong ? (int)A.flong[ro + q] : -1;
+            sv[u] = 1.0;
+            if (!FIRST && ok) sv[u] = A.fscale ? A.fscale[ro + q] : A.scale[rr[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < RQ; ++u) {
+            const int q = lane + 64 * u;
+            if (q < m) {
+                rm[q] = 0ull;
+                if (!FIRST) sl[q] = sv[u];
+            }
+        }
+    } else {
+        for (int q = lane; q < m; q += NT) {
+            rm[q] = 0ull;
+            if (!FIRST) sl[q] = A.scale[A.rows[ro + q]];
+        }
     }
     __syncthreads();
-    for (int64_t base = e0;;) {
+    for (int64_t base = e0; coal;) {
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            if (lp[u] == 0xffffffffu) continue;  // beyond the slot range
+            const int lr = (int)(lp[u] >> 16), lc = (int)(lp[u] & 0x7fffu);
+            double w = fabs(v[u]);
+            if (!FIRST) {
+                const double sr = sl[lr], sc = sl[lc];
+                w = (lp[u] & 0x8000u) ? sc * w * sr : sr * w * sc;
+            }
+            const unsigned long long bw = as_bits(w);
+            atomicMax(rm + lr, bw);
+            atomicMax(rm + lc, bw);
+        }
+        base += (int64_t)EB * NT;
+        if (base >= e1) break;  // uniform
+        load(base);
+    }
+    for (int64_t base = e0; !coal;) {
         int cc = -1;
         unsigned long long cm = 0ull;
 #pragma unroll
@@ -514,9 +564,21 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
         if (cc >= 0) atomicMax(rm + cc, cm);
         base += (int64_t)EB * NT;
         if (base >= e1) break;  // uniform
-        load(base + (int64_t)lane * EB);
+        load(base);
     }
     __syncthreads();
+    if (regrows) {
+#pragma unroll
+        for (int u = 0; u < RQ; ++u) {
+            const int q = lane + 64 * u;
+            if (q >= m) continue;
+            const unsigned long long bw = rm[q];
+            if (lk[u] >= 0) A.part_long[(int64_t)f * A.n_long + lk[u]] = as_double(bw);  // every front writes its slot
+            else if (A.diag_noatomic) A.part_long[rr[u] & 1023] = as_double(bw);  // diagnostics: timing without atomics
+            else if (bw != 0ull) atomicMax(A.rmax + rr[u], bw);
+        }
+        return;
+    }
     for (int q = lane; q < m; q += NT) {
         const int32_t r = A.rows[ro + q];
         const unsigned long long bw = rm[q];
@@ -1305,7 +1367,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
     for (int i = tid; i < m; i += NT) {
         const int32_t v = A.rows[ro + i];
         lrow[i] = v;
-        sloc[i] = A.scale[v];
+        sloc[i] = A.fscale ? A.fscale[ro + i] : A.scale[v];
     }
     for (int64_t t = tid; t < fsize; t += NT) st.F[t] = 0.0;
     __syncthreads();
@@ -3569,8 +3631,11 @@ static hipError_t launch_rowscanR(const ScanArgs& A, hipStream_t s) {
 // iters sweeps over the row-major copy.  The scalings live in the new numbering in A.scale_in / A.scale_out
 // (two scratch buffers of n doubles, the last sweep writes A.scale_out); A.scale (by original id) receives
 // the final one.
-hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s) {
-    if (A.n == 0) return hipSuccess;
+hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
+    if (A0.n == 0) return hipSuccess;
+    SweepArgs A = A0;
+    static const int noatomic = getenv("UNO_KKT_SWEEP_NOATOMIC") ? 1 : 0;  // diagnostics (wrong scaling)
+    A.diag_noatomic = noatomic;
     const size_t sh = 16 * (size_t)std::max(A.max_m, 1);
     const dim3 gn(grid_for(A.n, 256));
     hipError_t e = hipMemsetAsync(A.rmax, 0, sizeof(unsigned long long) * A.n, s);
@@ -3596,6 +3661,11 @@ hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s) {
             hipLaunchKernelGGL(k_sweep_long_fin, dim3(std::max(gl, 1u)), dim3(256), sizeof(unsigned long long) * A.n_long, s, A);
         }
         hipLaunchKernelGGL(k_sweep_update, gn, dim3(256), 0, s, A.rmax, A.scale, A.n, it == 0 ? 1 : 0);
+        // the scaling per front row for the next sweep (and, after the last one, for the factorization)
+        if (A.fscale) {
+            e = launch_front_scale(A.rows, A.scale, A.fscale, A.rows_total, s);
+            if (e != hipSuccess) return e;
+        }
     }
     if (iters == 0) hipLaunchKernelGGL(k_fill_ones, gn, dim3(256), 0, s, A.scale, A.n);  // the pass above only packed
     return hipGetLastError();
@@ -3661,7 +3731,8 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
     if (global) {
         return hipErrorInvalidValue;  // fronts beyond LDS: launch_big_* (host loop in kkt_api.cpp)
     } else {
-        size_t sh = factor_lds_bytes(mmax);
+        static const size_t lpad = getenv("UNO_KKT_LDS_PAD_LDS") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD_LDS")) : 0;  // diagnostics
+        size_t sh = factor_lds_bytes(mmax) + lpad;
         // small fronts: one wave per front (no cross-wave barriers, more fronts per CU);
         // larger fronts: four waves on a 16x16 update grid
         if (A.mf && mmax <= 64) {  // tile kernels (matrix-core trailing updates)
@@ -3731,6 +3802,18 @@ __global__ void k_reset_counters(unsigned long long* __restrict__ c) {
     const int t = threadIdx.x;
     if (t < kCounterSlots) c[t] = t == 8 ? ~0ull : 0ull;
 }
+__global__ void k_front_scale(const int32_t* __restrict__ rows, const double* __restrict__ scale, double* __restrict__ fscale,
+                              int64_t total) {
+    for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (int64_t)gridDim.x * blockDim.x)
+        fscale[t] = scale[rows[t]];
+}
+
+hipError_t launch_front_scale(const int32_t* rows, const double* scale, double* fscale, int64_t total, hipStream_t s) {
+    if (total <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_front_scale, dim3(grid_for(total, 256)), dim3(256), 0, s, rows, scale, fscale, total);
+    return hipGetLastError();
+}
+
 hipError_t launch_reset_counters(unsigned long long* counters, hipStream_t s) {
     hipLaunchKernelGGL(k_reset_counters, dim3(1), dim3(64), 0, s, counters);
     return hipGetLastError();
@@ -3816,7 +3899,10 @@ hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     if (A.df_nf <= 0) return hipSuccess;
     static const size_t pad = getenv("UNO_KKT_LDS_PAD") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD")) : 0;  // diagnostics
     if (A.mf && mmax <= 64) hipLaunchKernelGGL(k_factor_df_mf<4>, dim3(A.df_nf), dim3(64), factor_lds_bytes_mf(mmax) + pad, s, A);
-    else hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax), s, A);
+    else {
+        static const size_t lpad = getenv("UNO_KKT_LDS_PAD_LDS") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD_LDS")) : 0;  // diagnostics
+        hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax) + lpad, s, A);
+    }
     return hipGetLastError();
 }
 

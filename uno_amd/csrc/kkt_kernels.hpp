@@ -26,6 +26,7 @@ struct FactorArgs {
     const uint32_t* ent_lpos;   // (lr << 16) | flip << 15 | lc (flip: scale the column's side first)
     const double* uval;         // packed summed values
     const double* scale;        // equilibration, by original id
+    const double* fscale;       // the same gathered per front row (layout of rows; k_front_scale), or nullptr
     const int32_t* child_off;   // nf+1
     const int32_t* child;
     const int32_t* ch_cm;       // per child edge (aligned with child): contribution-block order
@@ -162,6 +163,11 @@ struct SweepArgs {
     int32_t n_long;
     double* part_long;          // nf * n_long
     int max_m;
+    int coalesced = 1;          // slot loads lane-contiguous (see k_sweep_front)
+    int diag_noatomic = 0;      // diagnostics only
+    double* fscale = nullptr;   // per front row (layout of rows): scale[rows[t]], refreshed after every sweep
+    int64_t rows_total = 0;     // front rows (length of rows / fscale / flong)
+    const int8_t* flong = nullptr;  // per front row: longpos of its row (-1: not a long row); nullptr: no long rows
     const int32_t* big_list;    // fronts of more than kSweepBigSlots slots (swept by 2-D grids)
     int32_t n_big = 0, big_slices = 1;
 };
@@ -222,6 +228,9 @@ hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, co
 // the factorization's device counter block: [0..7] pivot counters, [8] min pivot bits, [9] ||A_pre||_inf bits
 constexpr int kCounterSlots = 10;
 hipError_t launch_reset_counters(unsigned long long* counters, hipStream_t s);
+// fscale[t] = scale[rows[t]] for every front row t (one gather after the equilibration: the front assembly then
+// loads its rows' scalings in the same round trip as the row ids instead of after them)
+hipError_t launch_front_scale(const int32_t* rows, const double* scale, double* fscale, int64_t total, hipStream_t s);
 hipError_t launch_rhs_scale(const double* b, const double* scale, double* w, int64_t n, hipStream_t s);
 hipError_t launch_unscale(const double* w, const double* scale, double* x, int64_t n, hipStream_t s);
 hipError_t launch_solve(const SolveArgs& A, const int32_t* fronts, int count, int mmax, int pmax, bool forward,
