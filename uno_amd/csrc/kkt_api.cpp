@@ -207,6 +207,7 @@ struct uno_kkt {
     int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
                                  // factorization (1), also before every sweep (2)
     int sweep_coalesced = 1;     // option "sweep_coalesced"
+    int wpe2 = 0;                // option "wpe2"
     DBuf<double> fscale;
     DBuf<int8_t> flong;          // per front row: index of its row among the long rows, -1 otherwise
     int dff_enabled = 1;  // 0 off, 1 (default) levels >= L*, 2 also the small fronts below them (measured no faster at C3)
@@ -1260,6 +1261,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
     A.mf = h->mfma_fronts;
+    A.wpe2 = h->wpe2;
     A.big = h->big.p;
     if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
@@ -1448,6 +1450,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
     else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
+    else if (n == "wpe2") h->wpe2 = value != 0.0;
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;
     else if (n == "dist_force") h->dist_force = value != 0.0;

@@ -886,7 +886,12 @@ __device__ __forceinline__ void reg_load(const S& st, int m, double (&R)[MR][MR]
 #pragma unroll
         for (int b = 0; b <= a; ++b) {
             const int j = tx + G * b;
-            R[a][b] = st.F[(i < m && j <= i) ? st.idx(i, j) : -1];
+            const bool in = i < m && j <= i;
+            const double v = st.F[in ? st.idx(i, j) : -1];
+            // padding rows (i >= m) and the upper-triangle slots of diagonal blocks hold 0: the one-wave
+            // pivot step then needs no row-validity masks (a zero row never fails the test, publishes 0
+            // and is updated by 0)
+            R[a][b] = in ? v : 0.0;
         }
     }
 }
@@ -942,6 +947,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // the LDS step below (search, interchanges, 1x1/2x2/null, Schur update) and reloads
     double R[RM][RM];
     double* colv = coefB;  // free until the write-out
+    // one-wave register path: the published column gets its own G * RM doubles after the piv bytes (the
+    // slack factor_lds_bytes reserves), so padding rows can be stored unmasked
+    double* colw = coefB + 2 * m + (m + 7) / 8 + 1;
     // one-wave register path: columns whose L was written during the pivot loop (wave-uniform);
     // cleared by any later symmetric interchange (their rows moved: rewritten from LDS at the end)
     unsigned long long fastmask = 0;
@@ -971,24 +979,16 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     const double akk = readlane_d(R[bk][bk], kk * G + kk);
                     const double aak = fabs(akk);
                     const double dinv = 1.0 / akk;  // issued before the test: overlaps it
-                    // branch-free: every lane stores (non-owners into the trash slot F[-1]) and
-                    // reduces its candidates' |a_ik| with a max tree; u * max > |a_kk| is exactly
-                    // "some u |a_ik| > |a_kk|" (rounding of u * x is monotonic in x)
-                    double mx[RM];
+                    // the owners (tx == kk) publish column k (padding rows are 0: stored as is) and test
+                    // each candidate: "some u |a_ik| > |a_kk|" is exactly u * max_i |a_ik| > |a_kk| (the
+                    // rounding of u * x is monotonic in x); rows <= k of the diagonal block are excluded
+                    bool bad = false;
+                    if (owner) {
 #pragma unroll
-                    for (int a = 0; a < RM; ++a) {
-                        mx[a] = 0.0;
-                        if (a < bk) continue;
-                        const int i = ty + G * a;
-                        double* dst = (owner && i < m) ? colv + i : st.F - 1;  // colv has m entries
-                        *dst = R[a][bk];
-                        mx[a] = ((a > bk || i > k) && i < m) ? fabs(R[a][bk]) : 0.0;
+                        for (int a = bk; a < RM; ++a) colw[ty + G * a] = R[a][bk];
+#pragma unroll
+                        for (int a = bk; a < RM; ++a) bad |= (a > bk || ty > kk) && A.u * fabs(R[a][bk]) > aak;
                     }
-#pragma unroll
-                    for (int w = 1; w < RM; w *= 2)
-#pragma unroll
-                        for (int a = 0; a + w < RM; a += 2 * w) mx[a] = fmax(mx[a], mx[a + w]);
-                    const bool bad = owner && A.u * mx[0] > aak;
                     need = (__ballot(bad) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange
@@ -996,9 +996,8 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                         double lv[RM], cv[RM];
 #pragma unroll
                         for (int a = bk; a < RM; ++a) {
-                            // rows / columns >= m read slack beyond colv: only scratch registers use them
-                            lv[a] = colv[ty + G * a];
-                            cv[a] = colv[tx + G * a] * dinv;
+                            lv[a] = colw[ty + G * a];
+                            cv[a] = colw[tx + G * a] * dinv;
                         }
                         if (tx <= kk) cv[bk] = 0.0;  // columns <= k keep their values
 #pragma unroll
@@ -1469,8 +1468,8 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 // LDS layout of one front: [FrontShared 32 B][packed lower m(m+1)/2, even][sloc m][coefB m]
 // [lrow m][rstage/lorig m][piv m]
 
-template <int NT, int MR>
-__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MR > 8 ? 2 : 3))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
+template <int NT, int MR, int WPE = (MR > 8 ? 2 : 3)>
+__global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
     const int f = fronts[blockIdx.x];
@@ -1497,8 +1496,8 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(MR > 8 ? 2 :
 // reads their contribution blocks with sc1 loads, factors, writes its own contribution block with sc1
 // stores and, after the wave's vmcnt(0), adds one to its parent's counter.  Children factored by the
 // earlier level launches are complete before the launch.
-template <int MR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_factor_df(FactorArgs A) {
+template <int MR, int WPE = 3>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_factor_df(FactorArgs A) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
     uint32_t tk = 0;
@@ -3716,7 +3715,9 @@ hipError_t launch_scale(ScanArgs A, int iters, double* rmax, double* rowsum, hip
 size_t factor_lds_bytes(int mmax) {
     const size_t packed = (((size_t)mmax * (mmax + 1) / 2) + 1) & ~(size_t)1;
     // + slack: the register path reads the column vector (coefB) unclamped up to 2*kThreads... entries
-    const int grid_rows = mmax <= 32 ? 32 : (mmax <= 64 ? 64 : (mmax <= kMaxWaveFront ? kMaxWaveFront : 2 * kThreads));
+    // (the one-wave kernels publish the pivot column into G * RM doubles there: 64 for MR <= 8, also when
+    // the dataflow kernel k_factor_df<8> runs fronts of <= 32 rows)
+    const int grid_rows = mmax <= 64 ? 64 : (mmax <= kMaxWaveFront ? kMaxWaveFront : 2 * kThreads);
     return 32 + packed * sizeof(double) + 2 * (size_t)mmax * sizeof(double) + 2 * (size_t)mmax * sizeof(int32_t) +
            (size_t)((mmax + 15) & ~15) + (size_t)grid_rows * sizeof(double);
 }
@@ -3742,6 +3743,7 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
             if (mmax <= 32) hipLaunchKernelGGL((k_factor_mf<2>), dim3(count), dim3(64), sh, s, A, fronts);
             else hipLaunchKernelGGL((k_factor_mf<4>), dim3(count), dim3(64), sh, s, A, fronts);
         } else if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
+        else if (mmax <= 64 && A.wpe2) hipLaunchKernelGGL((k_factor_lds<64, 8, 2>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= 64) hipLaunchKernelGGL((k_factor_lds<64, 8>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= kMaxWaveFront) hipLaunchKernelGGL((k_factor_lds<64, 9>), dim3(count), dim3(64), sh, s, A, fronts);
         else hipLaunchKernelGGL((k_factor_lds<kThreads, 8>), dim3(count), dim3(kThreads), sh, s, A, fronts);
@@ -3901,7 +3903,8 @@ hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     if (A.mf && mmax <= 64) hipLaunchKernelGGL(k_factor_df_mf<4>, dim3(A.df_nf), dim3(64), factor_lds_bytes_mf(mmax) + pad, s, A);
     else {
         static const size_t lpad = getenv("UNO_KKT_LDS_PAD_LDS") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD_LDS")) : 0;  // diagnostics
-        hipLaunchKernelGGL(k_factor_df<8>, dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax) + lpad, s, A);
+        if (A.wpe2) hipLaunchKernelGGL((k_factor_df<8, 2>), dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax) + lpad, s, A);
+        else hipLaunchKernelGGL((k_factor_df<8>), dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax) + lpad, s, A);
     }
     return hipGetLastError();
 }
