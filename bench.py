@@ -324,6 +324,17 @@ def main():
         s_elapsed, s_inertia = timed_steps(sstep, args.steps, args.warmup, torch.cuda.synchronize, 1, dev)
         sst = ks.stats()
         xsv = xs_d.cpu().numpy()
+        # normwise backward error eta = |b - A x|_inf / (|A|_inf |x|_inf + |b|_inf) with and without the refinement step
+        anorm_inf = float(uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max())
+        def eta(xv):
+            return float(np.abs(uno_amd.coo_symv(n, rows, cols, vals, xv) - rhs).max() /
+                         (anorm_inf * np.abs(xv).max() + np.abs(rhs).max()))
+        eta_refined = eta(xsv)
+        ks.set_option("refine", 0)
+        ks.solve_device(rhs_d.data_ptr(), xs_d.data_ptr())
+        torch.cuda.synchronize()
+        eta_unrefined = eta(xs_d.cpu().numpy())
+        ks.set_option("refine", 1)
         sres = np.abs(uno_amd.coo_symv(n, rows, cols, vals, xsv) - rhs).max()
         sabs = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max()
         shipped = {"value": round(args.steps / s_elapsed, 4), "unit": "factor+solve/s",
@@ -333,6 +344,7 @@ def main():
                    "pivots_relaxed": sst["pivots_relaxed"], "fronts_merged": sst["fronts_merged"],
                    "refinement_steps_per_solve": 1 if sst["pivots_relaxed"] > 0 else 0,
                    "inertia": list(s_inertia), "inertia_equal_to_headline": tuple(s_inertia) == tuple(inertia),
+                   "backward_error_unrefined": eta_unrefined, "backward_error_refined": eta_refined,
                    "rel_residual": float(sres / (sabs * np.abs(xsv).max() + np.abs(rhs).max()))}
         del ks
 

@@ -1262,6 +1262,8 @@ int enqueue_factorization(uno_kkt_t h) {
     A.fmin = h->fmin.p;
     A.mf = h->mfma_fronts;
     A.wpe2 = h->wpe2;
+    static const int diag_nopiv = getenv("UNO_KKT_DIAG_NOPIV") ? atoi(getenv("UNO_KKT_DIAG_NOPIV")) : 0;
+    A.diag_nopiv = diag_nopiv;
     A.big = h->big.p;
     if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;

@@ -959,6 +959,12 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         if (W > 1 && tid == 0) sh->failk = -1;
         reg_load<G, RM>(st, m, R);
     }
+    if (A.diag_nopiv) {  // timing diagnostics only: no pivot steps (every column written as a 1x1 pivot)
+        for (int i = tid; i < p; i += NT) piv[i] = PIV_1X1;
+        __syncthreads();
+        k = p;
+        spilled = true;
+    }
     while (k < p) {
         if constexpr (REG && W == 1) {
             // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of

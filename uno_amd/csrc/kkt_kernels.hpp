@@ -56,6 +56,7 @@ struct FactorArgs {
     double u;
     double null_fac;
     int mf;                     // 1: one-wave fronts on the matrix-core tile kernels (k_factor_mf / k_factor_df_mf)
+    int diag_nopiv;             // diagnostics (env UNO_KKT_DIAG_NOPIV): fronts factored with p = 0 (timing only)
     int wpe2;                   // the m <= 64 register kernels built for 2 waves per SIMD (256 VGPRs) instead of 3
     // dataflow schedule of the upper tree (k_factor_df), after the level launches of the lower levels
     const int32_t* df_order;    // fronts, children before parents
