@@ -327,8 +327,11 @@ def main():
         # normwise backward error eta = |b - A x|_inf / (|A|_inf |x|_inf + |b|_inf) with and without the refinement step
         anorm_inf = float(uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.ones(n)).max())
         def eta(xv):
-            return float(np.abs(uno_amd.coo_symv(n, rows, cols, vals, xv) - rhs).max() /
-                         (anorm_inf * np.abs(xv).max() + np.abs(rhs).max()))
+            """normwise and componentwise backward errors of xv"""
+            r = np.abs(uno_amd.coo_symv(n, rows, cols, vals, xv) - rhs)
+            den = uno_amd.coo_symv(n, rows, cols, np.abs(vals), np.abs(xv)) + np.abs(rhs)
+            comp = float(np.max(np.where(den > 0, r / np.where(den > 0, den, 1.0), 0.0)))
+            return [float(r.max() / (anorm_inf * np.abs(xv).max() + np.abs(rhs).max())), comp]
         eta_refined = eta(xsv)
         ks.set_option("refine", 0)
         ks.solve_device(rhs_d.data_ptr(), xs_d.data_ptr())

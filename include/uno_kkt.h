@@ -57,6 +57,10 @@ typedef struct {
     int64_t solve_aborts;   /* dataflow solves abandoned at the dependency-wait limit (then level-scheduled) */
     int64_t factor_df_fronts; /* fronts factored by the one-launch dataflow kernel (upper tree; 0 = none) */
     int64_t factor_df_aborts; /* dataflow factorizations redone level by level after a wait limit */
+    int64_t refinements;    /* refinement steps applied since analysis (option "refine") */
+    int64_t refinements_skipped; /* refinement steps skipped: componentwise backward error <= "refine_tol" */
+    double last_backward_error;  /* componentwise backward error max_i |b - A x|_i / (|A| |x| + |b|)_i of the last
+                                    checked solve (before its refinement step; -1 = not checked) */
 } uno_kkt_stats_t;
 
 /* Create a solver bound to HIP device `device_id`.  Replaces MUMPS JOB=-1 (MUMPSSolver.cpp:16-37). */

@@ -228,6 +228,7 @@ def test_hipldl_plugin_arrowband_1e5():
 
 
 C3_GOLDEN = os.path.join(ROOT, "tests", "golden", "arrowband1000000_uno_oracle.json")
+C3_GOLDEN_CM = os.path.join(ROOT, "tests", "golden", "arrowband1000000_uno_oracle_cm.json")
 
 
 def rounding_tie(c, sigma_rel=1e-10):
@@ -236,50 +237,45 @@ def rounding_tie(c, sigma_rel=1e-10):
     return any(sh["sigma_rel"] <= sigma_rel * (1 + 1e-9) and sh["oracle_plus"] != sh["oracle_minus"] for sh in c["shifts"])
 
 
+def test_c3_golden_traces_part_at_a_rounding_tie():
+    """The two reference runs at configs[2] (tests/golden/make_c3_golden.sh: the CPU oracle with the reverse
+    Cuthill-McKee ordering, and with Cuthill-McKee) are both correct MUMPS-semantics solves whose iterate
+    sequences part at factorization 1051: 589 / 1 465 vs 588 / 1 467 iterations / factorizations, the same
+    solution."""
+    g, c = json.load(open(C3_GOLDEN)), json.load(open(C3_GOLDEN_CM))
+    assert g["status"] == c["status"] == 0
+    a, b = g["inertia_trace"], c["inertia_trace"]
+    assert next(i for i, (x, y) in enumerate(zip(a, b)) if x != y) == 1051
+    assert (g["iterations"], g["factorizations"]) == (589, 1465) and (c["iterations"], c["factorizations"]) == (588, 1467)
+    assert abs(g["objective"] - c["objective"]) <= 1e-12 * abs(g["objective"])
+
+
 @needs_driver
 @pytest.mark.gpu
 @pytest.mark.timeout(1000)
 def test_hipldl_plugin_arrowband_1e6(tmp_path):
-    """north_star at the headline size, configs[2]: KKT dimension 1e6, nnz 2e7, 589 ipopt-preset iterations and
-    1 465 factorizations in the golden run (the ORACLE run of tests/golden/make_c3_golden.sh, container CPU time).
-
-    What is required, and why not an identical trace ("Whole solve at 1e6"):
-    - the GPU plugin's run reproduces the golden trace exactly -- every factorization's inertia -- up to the
-      first factorization where the two differ, which must come late (after 1 000 of them);
-    - at that factorization, and at the first one where the two runs' inertia-correction decisions part, the
-      driver re-factors the GPU run's own matrix with the CPU oracle: the oracle must report the GPU's inertia
-      (the GPU factorization is right for its input), and at the first difference the shift ladder must show an
-      eigenvalue within 1e-10 ||A||_inf of zero (the count there is decided by the rounding of the iterate, not
-      by the factorization: two correct solvers on trajectories that agree to rounding may count it either way);
-    - the solve converges like the golden run: status, iteration count within 3, objective within 1e-10
-      relative, the primal summaries within 1e-9, every multiplier summary within 1e-6 and the final primal /
-      dual residual measures (Iterate.hpp:43-46) within 10 % of the golden run's or below 1e-10."""
-    g = json.load(open(C3_GOLDEN))
-    assert g["status"] == 0 and g["iterations"] > 100
+    """north_star at the headline size, configs[2]: KKT dimension 1e6, nnz 2e7.  The reference Uno core with
+    the CPU oracle has two valid iterate sequences here, one per oracle ordering (the reverse Cuthill-McKee run,
+    589 iterations / 1 465 factorizations, and the Cuthill-McKee run, 588 / 1 467; they part at factorization
+    1051 where the matrix has an eigenvalue within 1e-10 ||A||_inf of zero).  The GPU plugin must reproduce
+    one of them exactly -- iterations, factorization and solve counts, every factorization's inertia -- with
+    objective, primal summaries, every multiplier summary and the final residual measures within 1e-10
+    relative (same_large_run).  Where it leaves the reverse Cuthill-McKee trace, the driver re-factors the GPU
+    run's own matrix with the oracle (UNO_KKT_CROSSCHECK_TRACE): same inertia as the GPU, and the shift
+    ladder shows the rounding-level eigenvalue."""
+    g, gc = json.load(open(C3_GOLDEN)), json.load(open(C3_GOLDEN_CM))
     trace = tmp_path / "golden_trace.txt"
     trace.write_text("".join(f"{p} {q} {z}\n" for _, p, q, z in g["inertia_trace"]))
     r = drive(["arrowband:1000000", "linear_solver=HIPLDL"], 950, env={"UNO_KKT_CROSSCHECK_TRACE": str(trace)})
-    assert r["status"] == g["status"] == 0
-    a, b = r["inertia_trace"], g["inertia_trace"]
-    first = next((i for i, (x, y) in enumerate(zip(a, b)) if x != y), min(len(a), len(b)))
-    if first == len(a) == len(b):  # identical trace: the strict bar
-        same_large_run(r, g)
-        return
-    assert first >= 1000, f"the GPU trace leaves the golden one at factorization {first}"
-    checks = {c["index"]: c for c in r["crosscheck"]}
-    assert first in checks, r["crosscheck"]
-    for c in r["crosscheck"]:
-        assert c["oracle"] == c["run_inertia"] == c["gpu"], c  # GPU factorization == oracle on the same matrix
-    assert rounding_tie(checks[first]), checks[first]
-    assert abs(r["iterations"] - g["iterations"]) <= 3
-    assert abs(r["objective"] - g["objective"]) <= 1e-10 * abs(g["objective"])
-    for x, y in zip(r["primals_summary"], g["primals_summary"]):
-        assert abs(x - y) <= 1e-9 * max(1.0, abs(y)), ("primals_summary", x, y)
-    for key in DUALS:
-        for x, y in zip(r[key + "_summary"], g[key + "_summary"]):
-            assert abs(x - y) <= 1e-6 * max(1.0, abs(y)), (key, x, y)
-    for x, y in zip(r["residuals"], g["residuals"]):
-        assert x <= max(1.1 * y, 1e-10), ("residuals", r["residuals"], g["residuals"])
+    match = g if r["inertia_trace"] == g["inertia_trace"] else gc
+    same_large_run(r, match)
+    if match is gc:
+        first = next(i for i, (x, y) in enumerate(zip(r["inertia_trace"], g["inertia_trace"])) if x != y)
+        checks = {c["index"]: c for c in r["crosscheck"]}
+        assert first in checks, r["crosscheck"]
+        for c in r["crosscheck"]:
+            assert c["oracle"] == c["run_inertia"] == c["gpu"], c  # GPU factorization == oracle on the same matrix
+        assert rounding_tie(checks[first]), checks[first]
 
 
 @needs_driver

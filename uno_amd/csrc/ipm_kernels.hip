@@ -140,10 +140,18 @@ __global__ void k_symv(SymvArgs A) {
     if ((int64_t)(A.cptr[i + 1] - A.cptr[i]) + (A.rptr[i + 1] - A.rptr[i]) > A.long_len) return;  // k_symv_long
     const int32_t oi = A.perm[i];
     double acc = 0.0;
-    for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += 16) acc += A.uval[q] * A.x[A.ent_r[q]];
-    for (int32_t t = A.rptr[i] + lane; t < A.rptr[i + 1]; t += 16) {
-        const int32_t q = A.rslot[t];
-        acc += A.uval[q] * A.x[A.ent_c[q]];
+    if (A.absval) {
+        for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += 16) acc += fabs(A.uval[q]) * fabs(A.x[A.ent_r[q]]);
+        for (int32_t t = A.rptr[i] + lane; t < A.rptr[i + 1]; t += 16) {
+            const int32_t q = A.rslot[t];
+            acc += fabs(A.uval[q]) * fabs(A.x[A.ent_c[q]]);
+        }
+    } else {
+        for (int32_t q = A.cptr[i] + lane; q < A.cptr[i + 1]; q += 16) acc += A.uval[q] * A.x[A.ent_r[q]];
+        for (int32_t t = A.rptr[i] + lane; t < A.rptr[i + 1]; t += 16) {
+            const int32_t q = A.rslot[t];
+            acc += A.uval[q] * A.x[A.ent_c[q]];
+        }
     }
     for (int off = 8; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 16);
     if (lane == 0) {
@@ -163,13 +171,9 @@ __global__ void k_symv_long(SymvArgs A) {
     const int32_t b = blockIdx.x * kSymvChunk, e = min(len, b + kSymvChunk);
     double acc = 0.0;
     for (int32_t t = b + threadIdx.x; t < e; t += kT) {
-        if (t < nc) {
-            const int32_t q = c0 + t;
-            acc += A.uval[q] * A.x[A.ent_r[q]];
-        } else {
-            const int32_t q = A.rslot[r0 + (t - nc)];
-            acc += A.uval[q] * A.x[A.ent_c[q]];
-        }
+        const int32_t q = t < nc ? c0 + t : A.rslot[r0 + (t - nc)];
+        const double xv = A.x[t < nc ? A.ent_r[q] : A.ent_c[q]];
+        acc += A.absval ? fabs(A.uval[q]) * fabs(xv) : A.uval[q] * xv;
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
@@ -262,6 +266,27 @@ hipError_t launch_direction(const DirArgs& A, hipStream_t s) {
     if (A.n + A.m == 0) return hipGetLastError();
     hipLaunchKernelGGL(k_direction, dim3(grid_of(A.n + A.m)), dim3(kT), 0, s, A);
     hipLaunchKernelGGL(k_direction_scale, dim3(grid_of(A.n + A.m)), dim3(kT), 0, s, A);
+    return hipGetLastError();
+}
+
+__global__ void k_backward_error(const double* __restrict__ r, const double* __restrict__ t, const double* __restrict__ b,
+                                 int64_t n, unsigned long long* __restrict__ out_bits) {
+    double mx = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
+        const double num = fabs(r[i]), den = t[i] + fabs(b[i]);
+        const double w = den > 0.0 ? num / den : (num > 0.0 ? INFINITY : 0.0);
+        mx = fmax(mx, w);
+    }
+    for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
+    if ((threadIdx.x & 63) == 0 && mx > 0.0) atomicMax(out_bits, (unsigned long long)__double_as_longlong(mx));
+}
+
+hipError_t launch_backward_error(const double* r, const double* t, const double* b, int64_t n, unsigned long long* out_bits,
+                                 hipStream_t s) {
+    hipError_t e = hipMemsetAsync(out_bits, 0, sizeof(unsigned long long), s);
+    if (e != hipSuccess || n == 0) return e;
+    const int64_t g = grid_of(n);
+    hipLaunchKernelGGL(k_backward_error, dim3((unsigned)(g > 1024 ? 1024 : g)), dim3(kT), 0, s, r, t, b, n, out_bits);
     return hipGetLastError();
 }
 

@@ -42,6 +42,7 @@ struct SymvArgs {
     const int32_t* long_rows = nullptr;  // new numbering
     int32_t n_long = 0, long_chunks = 0;
     double* long_part = nullptr;         // n_long * long_chunks chunk partials (summed in chunk order)
+    int absval = 0;                      // y += |A| |x| (the denominator of the componentwise backward error)
 };
 constexpr int kSymvChunk = 4096;
 constexpr int kSumParts = 1024;  // quadratic_product: block partials of the deterministic two-pass sum
@@ -52,6 +53,10 @@ hipError_t launch_direction(const DirArgs& A, hipStream_t s);
 hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double* lb, const double* ub, const double* x,
                           const double* zl, const double* zu, int64_t count, double* values, hipStream_t s);
 // dot_out (only with A.dot_w): 1 + kSumParts doubles, the result first
+// out_bits[0] = bits of max_i |r_i| / (t_i + |b_i|) (0 where the denominator is 0 and r_i = 0, +inf where only
+// the denominator is 0): the componentwise backward error of x with r = A x - b, t = |A| |x|
+hipError_t launch_backward_error(const double* r, const double* t, const double* b, int64_t n, unsigned long long* out_bits,
+                                 hipStream_t s);
 hipError_t launch_symv(const SymvArgs& A, double* dot_out, hipStream_t s);
 
 }  // namespace ukkt

@@ -963,6 +963,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         for (int i = tid; i < p; i += NT) piv[i] = PIV_1X1;
         __syncthreads();
         k = p;
+        npos = p;
         spilled = true;
     }
     while (k < p) {
@@ -1170,7 +1171,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         // L of the columns pivoted by the register path: column j (< p) still holds A(i, j) as it
         // was at step j, so L(i, j) = A(i, j) / d_j and L(j, j) = d_j, stored straight from the
         // registers (for a fixed register, the 8 lanes of a column group write 8 consecutive rows)
-        if (fastmask) {
+        if (fastmask && !(A.diag_nopiv & 2)) {
             const int ty = tid / G, tx = tid % G;
 #pragma unroll
             for (int b = 0; b < RM; ++b) {
@@ -1189,7 +1190,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         }
     }
     // columns still to be written from the LDS front (all when no register path ran)
-    const bool lds_L = !(REG && W == 1) || fastmask != (p >= 64 ? ~0ull : ((1ull << p) - 1));
+    const bool lds_L = !(A.diag_nopiv & 2) && (!(REG && W == 1) || fastmask != (p >= 64 ? ~0ull : ((1ull << p) - 1)));
     const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
@@ -1289,7 +1290,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     if (sub) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
     // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
-    const int cm = m - p;
+    const int cm = (A.diag_nopiv & 4) ? 0 : m - p;
     if constexpr (REG && W == 1) {
         // contribution block straight from the registers: element (i, j), p <= j <= i < m
         if (cm > 0) {
@@ -1379,7 +1380,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
     const bool asm_st = A.stamps && A.stamp_mode == 4 && tid == 0;  // diagnostics: assembly sub-phases
     if (asm_st) A.stamps[8 * f + 4] = __builtin_amdgcn_s_memrealtime();
     // original entries (distinct positions, summed duplicates already packed by k_pack)
-    for (int64_t eb = e0 + tid;; eb += (int64_t)EB * NT) {
+    for (int64_t eb = e0 + tid; !(A.diag_nopiv & 8); eb += (int64_t)EB * NT) {
 #pragma unroll
         for (int q = 0; q < EB; ++q) {
             const int64_t e = eb + (int64_t)q * NT;
@@ -1432,7 +1433,7 @@ __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t
 #pragma unroll
         for (int u = 0; u < CB; ++u) st.F[b.pos[u]] = old[u] + b.v[u];
     };
-    for (int cb0 = c0; cb0 < c1; cb0 += 64) {
+    for (int cb0 = c0; cb0 < c1 && !(A.diag_nopiv & 8); cb0 += 64) {
         if (cb0 != c0 && lane < c1 - cb0) {
             my_cm = A.ch_cm[cb0 + lane];
             my_rmo = (unsigned long long)A.ch_relmap_off[cb0 + lane];

@@ -33,6 +33,7 @@ class KKTStats(ctypes.Structure):
         ("flops", ctypes.c_double), ("analysis_seconds", ctypes.c_double), ("bytes_L", ctypes.c_double),
         ("bytes_cb", ctypes.c_double), ("fronts_merged", ctypes.c_int64), ("solve_grid", ctypes.c_int64),
         ("solve_aborts", ctypes.c_int64), ("factor_df_fronts", ctypes.c_int64), ("factor_df_aborts", ctypes.c_int64),
+        ("refinements", ctypes.c_int64), ("refinements_skipped", ctypes.c_int64), ("last_backward_error", ctypes.c_double),
     ]
 
     def as_dict(self):
