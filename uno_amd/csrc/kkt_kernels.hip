@@ -1347,33 +1347,93 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
 // Latency-bound (a few KB per front), so the loads are grouped into as few dependent round trips as
 // possible: {rows, first entry batch, children's edge metadata} -> {scales} -> {per child: CB values
 // and both relmap entries of each element together}.
+// A front's offsets (scalar), and the first round trip of its assembly held in registers: the row ids and their
+// scalings (rows < 2 NT: every front of the LDS kernels), the first batch of its original entries and its
+// children's edge records.  asm_issue issues those loads, assemble_front_pre consumes them.  (Issuing them for the
+// next front under the current front's pivot loop, in a resident-grid kernel, measured slower at C3: 1.36 / 1.25 ms
+// vs 1.18 ms, 255-256 VGPRs with spills; round 3.)
+struct FrontMeta {
+    int m, p, c0, c1;
+    int64_t ro, e0, e1;
+};
+__device__ __forceinline__ FrontMeta front_meta(const FactorArgs& A, int f) {
+    FrontMeta r;
+    r.m = A.fm[f]; r.p = A.fp[f];
+    r.ro = A.rows_off[f];
+    r.e0 = A.ent_off[f]; r.e1 = A.ent_off[f + 1];
+    r.c0 = A.child_off[f]; r.c1 = A.child_off[f + 1];
+    return r;
+}
+constexpr int kAsmEB = 8;
+struct AsmPre {
+    uint32_t lp[kAsmEB];
+    double uv[kAsmEB];
+    int my_cm;
+    unsigned long long my_rmo, my_cbo;
+    int32_t r0, r1;
+    double s0, s1;
+};
+template <int NT>
+__device__ __forceinline__ void asm_issue_entries(AsmPre& q, const FactorArgs& A, const FrontMeta& M) {
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < kAsmEB; ++u) {
+        const int64_t e = M.e0 + tid + (int64_t)u * NT;
+        q.lp[u] = e < M.e1 ? A.ent_lpos[e] : 0u;
+        q.uv[u] = e < M.e1 ? A.uval[e] : 0.0;
+    }
+}
+template <int NT>
+__device__ __forceinline__ void asm_issue(AsmPre& q, const FactorArgs& A, const FrontMeta& M, bool with_scale) {
+    const int tid = threadIdx.x, lane = tid & 63;
+    asm_issue_entries<NT>(q, A, M);
+    q.my_cm = 0;
+    q.my_rmo = q.my_cbo = 0;
+    if (lane < M.c1 - M.c0) {
+        q.my_cm = A.ch_cm[M.c0 + lane];
+        q.my_rmo = (unsigned long long)A.ch_relmap_off[M.c0 + lane];
+        q.my_cbo = (unsigned long long)A.ch_cb_off[M.c0 + lane];
+    }
+    q.r0 = tid < M.m ? A.rows[M.ro + tid] : 0;
+    q.r1 = tid + NT < M.m ? A.rows[M.ro + tid + NT] : 0;
+    if (with_scale) {  // per-front-row scalings (A.fscale): same round trip as the row ids
+        q.s0 = tid < M.m ? A.fscale[M.ro + tid] : 0.0;
+        q.s1 = tid + NT < M.m ? A.fscale[M.ro + tid + NT] : 0.0;
+    }
+}
+
+template <int NT, bool DF, class S>
+__device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& M, int32_t* lrow, double* sloc,
+                                   AsmPre& q, const FactorArgs& A, int f);
+
 template <int NT, bool DF, class S>
 __device__ void assemble_front(const S& st, int64_t fsize, int m, int p, int32_t* lrow, double* sloc, int32_t* rstage,
                                const FactorArgs& A, int f) {
+    const FrontMeta M = front_meta(A, f);
+    AsmPre q;
+    asm_issue<NT>(q, A, M, A.fscale != nullptr);
+    assemble_front_pre<NT, DF>(st, fsize, M, lrow, sloc, q, A, f);
+}
+
+template <int NT, bool DF, class S>
+__device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& M, int32_t* lrow, double* sloc,
+                                   AsmPre& q, const FactorArgs& A, int f) {
     const int tid = threadIdx.x, lane = tid & 63;
-    const int64_t ro = A.rows_off[f];
-    const int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
-    const int c0 = A.child_off[f], c1 = A.child_off[f + 1];
-    constexpr int EB = 8;
-    uint32_t lp[EB];
-    double uv[EB];
-#pragma unroll
-    for (int q = 0; q < EB; ++q) {
-        const int64_t e = e0 + tid + (int64_t)q * NT;
-        lp[q] = e < e1 ? A.ent_lpos[e] : 0u;
-        uv[q] = e < e1 ? A.uval[e] : 0.0;
+    const int m = M.m;
+    const int64_t e0 = M.e0, e1 = M.e1;
+    const int c0 = M.c0, c1 = M.c1;
+    constexpr int EB = kAsmEB;
+    uint32_t (&lp)[EB] = q.lp;
+    double (&uv)[EB] = q.uv;
+    int my_cm = q.my_cm;
+    unsigned long long my_rmo = q.my_rmo, my_cbo = q.my_cbo;
+    if (tid < m) {
+        lrow[tid] = q.r0;
+        sloc[tid] = A.fscale ? q.s0 : A.scale[q.r0];
     }
-    int my_cm = 0;
-    unsigned long long my_rmo = 0, my_cbo = 0;
-    if (lane < c1 - c0) {
-        my_cm = A.ch_cm[c0 + lane];
-        my_rmo = (unsigned long long)A.ch_relmap_off[c0 + lane];
-        my_cbo = (unsigned long long)A.ch_cb_off[c0 + lane];
-    }
-    for (int i = tid; i < m; i += NT) {
-        const int32_t v = A.rows[ro + i];
-        lrow[i] = v;
-        sloc[i] = A.fscale ? A.fscale[ro + i] : A.scale[v];
+    if (tid + NT < m) {
+        lrow[tid + NT] = q.r1;
+        sloc[tid + NT] = A.fscale ? q.s1 : A.scale[q.r1];
     }
     for (int64_t t = tid; t < fsize; t += NT) st.F[t] = 0.0;
     __syncthreads();
