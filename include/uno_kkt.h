@@ -89,6 +89,10 @@ int uno_kkt_analyze(uno_kkt_t handle, int64_t n, int64_t nnz, const int64_t* row
 /* Numerical LDL^T factorization of the values in COO order (same order as the analysed pattern).
  * values_on_device = 0: host pointer (copied H2D), 1: device pointer, and values == NULL reuses the
  * device-resident values of the previous call (after uno_kkt_set_values / uno_kkt_fill_values).
+ * Asynchronous for patterns whose fronts all fit the LDS kernels (m <= 128): the call returns once the work
+ * is queued and uno_kkt_inertia / uno_kkt_solve synchronise.  A pattern with larger fronts blocks the host
+ * inside this call while those fronts factor (their panel steps are driven from the host, one stream sync
+ * per batch of steps).
  * Replaces do_numerical_factorization / JOB=2 (MUMPSSolver.cpp:85-89). */
 int uno_kkt_factorize(uno_kkt_t handle, const double* values, int values_on_device);
 
