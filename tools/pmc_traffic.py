@@ -12,8 +12,9 @@ fe, wr, out = (json.load(open(sys.argv[1])), json.load(open(sys.argv[2])), sys.a
 pf, pw = fe["per_run"], wr["per_run"]
 kb = 1024.0
 res = {
-    "source": "tools/profile_round.sh (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
-              "bench.py --steps 3 --warmup 1 --profile-only), summarised by tools/pmc_traffic.py",
+    "source": "tools/profile_r03.sh (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes, "
+              "bench.py --steps 6 --warmup 1 --profile-only), summarised by tools/rocpd_summary.py pmc_steady "
+              "and tools/pmc_traffic.py",
     "correction": "FETCH_SIZE doubled (gfx950: FETCH_SIZE tallies 1/2 of the bytes of wide streaming reads, "
                   "MI355X_MICROARCH.md HBM); WRITE_SIZE as reported; KB = 1024 B; the factor kernels' 8-byte gathers "
                   "are an uncalibrated access width, so the doubled figure is an upper bound",
@@ -23,8 +24,7 @@ res = {
     "factor_bytes_raw_fetch_plus_write": int(kb * (pf["factor"]["FETCH_SIZE"] + pw["factor"]["WRITE_SIZE"])),
     "solve_bytes_per_solve": int(kb * (pf["solve"]["FETCH_SIZE_x2"] + pw["solve"]["WRITE_SIZE"])),
     "solve_bytes_raw_fetch_plus_write": int(kb * (pf["solve"]["FETCH_SIZE"] + pw["solve"]["WRITE_SIZE"])),
-    "note": "factorization count includes the first call's delayed-pivot merge rounds (2 extra factorizations "
-            "on intermediate structures)",
+    "note": fe.get("note", ""),
 }
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps(res, indent=1))

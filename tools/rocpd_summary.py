@@ -62,6 +62,41 @@ def pmc(db, out):
     print(json.dumps(res, indent=1))
 
 
+def pmc_steady(db, out, skip=3):
+    """As `pmc`, but per factorization / solve of the steady state only: dispatches are split into
+    factorizations at every k_reset_counters dispatch (the first kernel of a factorization) and the first
+    `skip` of them (warm-up, the first call's delayed-pivot merge rounds) are dropped."""
+    c = sqlite3.connect(db)
+    rows = c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection "
+                     "order by dispatch_id").fetchall()
+    starts = sorted({d for d, k, _, _ in rows if "k_reset_counters" in k})
+    import bisect
+    res = {"per_run": {}, "factorizations": max(0, len(starts) - skip), "solves": 0,
+           "note": f"steady state: factorizations after the first {skip} (k_reset_counters dispatches); KB per "
+                   "factorization, solve group per solve; FETCH_SIZE_x2 applies the gfx950 1/2 correction"}
+    solves = set()
+    acc = {}
+    for d, k, cn, v in rows:
+        gi = bisect.bisect_right(starts, d) - 1
+        if gi < skip:
+            continue
+        g = group_of(k)
+        if g == "solve":
+            solves.add(d if "k_solve_fwd" in k else None)
+        acc.setdefault(g, {}).setdefault(cn, 0.0)
+        acc[g][cn] += v
+    nsol = len([x for x in solves if x is not None])
+    res["solves"] = nsol
+    nfac = max(1, res["factorizations"])
+    for g, d in acc.items():
+        runs = max(1, nsol if g == "solve" else nfac)
+        res["per_run"][g] = {cn: v / runs for cn, v in d.items()}
+        if "FETCH_SIZE" in d:
+            res["per_run"][g]["FETCH_SIZE_x2"] = 2 * d["FETCH_SIZE"] / runs
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def bykernel(db):
     """per kernel name: every counter summed over its dispatches, divided by the dispatch count"""
     c = sqlite3.connect(db)
@@ -76,6 +111,9 @@ def bykernel(db):
 
 
 if __name__ == "__main__":
+    if sys.argv[1] == "pmc_steady":
+        pmc_steady(sys.argv[2], sys.argv[3])
+        sys.exit(0)
     if sys.argv[1] == "bykernel":
         bykernel(sys.argv[2])
     elif sys.argv[1] == "stats":
