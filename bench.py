@@ -228,7 +228,8 @@ def main():
         except Exception as e:  # noqa: BLE001 -- reported, then the replicas mode runs
             ok, err = 0, repr(e)[:300]
         flag = torch.tensor([ok], dtype=torch.int32, device=dev)
-        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        if world > 1:
+            dist.all_reduce(flag, op=dist.ReduceOp.MIN)
         if int(flag.item()) == 0:
             dist_fallback = err or "another rank failed"
             dist_mode = False

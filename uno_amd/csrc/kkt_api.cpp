@@ -204,6 +204,8 @@ struct uno_kkt {
     // dataflow factorization of the upper tree (levels >= dff_level, every front one-wave); option
     // "dataflow_factor" (default 1)
     int concurrent_classes = 1;  // option "concurrent_classes"
+    int early_xpos = 1;          // option "early_xpos": the dataflow solve's row maps queued with the factorization
+    hipEvent_t ev_counters = nullptr;  // after the counters' read-back of the last enqueued factorization
     int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
                                  // factorization (1), also before every sweep (2)
     int sweep_coalesced = 1;     // option "sweep_coalesced"
@@ -682,7 +684,7 @@ int allreduce_host(uno_kkt_t h, std::vector<unsigned long long>& v, RedOp op) {
 // wait for the factorization; if it ran with the overlapped norm (threshold 0), check that no
 // accepted pivot is at or below the exact null-pivot threshold, else refactor with the exact one
 int sync_and_verify(uno_kkt_t h) {
-    HIPCHK(h, hipStreamSynchronize(h->stream));
+    HIPCHK(h, hipEventSynchronize(h->ev_counters));  // the counters (and the dataflow abort word) are on the host
     uint32_t ab = 0;
     memcpy(&ab, h->h_counters + 11, sizeof(ab));
     if (ab != 0) {
@@ -1189,6 +1191,22 @@ int upload_structure(uno_kkt_t h) {
     return UNO_KKT_OK;
 }
 
+// rxpos / xpos of the dataflow solve for the factorization just enqueued (they depend on its pivoting, not on
+// the right-hand side): queued right behind the counters' read-back, so they run while the host checks the
+// inertia instead of at the start of the next solve (one GPU)
+hipError_t enqueue_xpos(uno_kkt_t h) {
+    if (h->world != 1 || !h->df_enabled || h->df_grid <= 0 || !h->early_xpos) return hipSuccess;
+    SolveArgs A;
+    A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
+    A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
+    A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p; A.ch_cm = h->ch_cm.p;
+    A.ch_relmap_off = h->ch_relmap_off.p;
+    const DfArgs Df = dataflow_args(h);
+    hipError_t e = launch_xpos(A, Df, h->df_xpos.p, h->df_rxpos.p, nullptr, 0, h->df_top_base, h->stream);
+    if (e == hipSuccess) h->df_rx_valid = true;
+    return e;
+}
+
 int enqueue_factorization(uno_kkt_t h) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
@@ -1356,8 +1374,10 @@ int enqueue_factorization(uno_kkt_t h) {
     }
     // counters and minbits in one copy (h_counters[8] is the min pivot bits)
     HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    HIPCHK(h, hipEventRecord(h->ev_counters, s));  // sync_and_verify waits for this, not for the xpos below
     h->factor_enqueued = true;
     h->df_rx_valid = false;  // pivoting may have permuted rows
+    HIPCHK(h, enqueue_xpos(h));
     return UNO_KKT_OK;
 }
 
@@ -1385,6 +1405,7 @@ int uno_kkt_create(uno_kkt_t* handle, int device_id) {
         hipEventCreateWithFlags(&h->ev_join4, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_scale, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_norm, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_counters, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc((void**)&h->h_big, sizeof(int32_t)) != hipSuccess) {
         delete h;
@@ -1421,6 +1442,7 @@ void uno_kkt_destroy(uno_kkt_t h) {
     if (h->stream2) hipStreamSynchronize(h->stream2);
     if (h->ev_scale) hipEventDestroy(h->ev_scale);
     if (h->ev_norm) hipEventDestroy(h->ev_norm);
+    if (h->ev_counters) hipEventDestroy(h->ev_counters);
     if (h->stream2) hipStreamDestroy(h->stream2);
     if (h->stream3) { hipStreamSynchronize(h->stream3); hipStreamDestroy(h->stream3); }
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
@@ -1457,6 +1479,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "overlap_norm") h->overlap_norm = value != 0.0;
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
+    else if (n == "early_xpos") h->early_xpos = value != 0.0;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
     else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
     else if (n == "wpe2") h->wpe2 = value != 0.0;
