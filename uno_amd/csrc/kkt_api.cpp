@@ -206,6 +206,9 @@ struct uno_kkt {
     int concurrent_classes = 1;  // option "concurrent_classes"
     int early_xpos = 1;          // option "early_xpos": the dataflow solve's row maps queued with the factorization
     hipEvent_t ev_counters = nullptr;  // after the counters' read-back of the last enqueued factorization
+    hipEvent_t ev_wait = nullptr;      // host_wait_stream
+    int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
+    bool rmax_clean = false;           // rmax all zero (left so by the front sweeps)
     int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
                                  // factorization (1), also before every sweep (2)
     int sweep_coalesced = 1;     // option "sweep_coalesced"
@@ -683,8 +686,26 @@ int allreduce_host(uno_kkt_t h, std::vector<unsigned long long>& v, RedOp op) {
 
 // wait for the factorization; if it ran with the overlapped norm (threshold 0), check that no
 // accepted pivot is at or below the exact null-pivot threshold, else refactor with the exact one
+// Host wait for an event.  Option "spin_wait" (default 1) polls it: hipEventSynchronize falls back to an
+// interrupt wait once the GPU has run for a while, and its wake-up adds tens of microseconds to every
+// factorization and solve (measured r03, tools/timeline.py)
+hipError_t host_wait(uno_kkt_t h, hipEvent_t ev) {
+    if (!h->spin_wait) return hipEventSynchronize(ev);
+    for (;;) {
+        const hipError_t e = hipEventQuery(ev);
+        if (e != hipErrorNotReady) return e;
+        __builtin_ia32_pause();
+    }
+}
+
+hipError_t host_wait_stream(uno_kkt_t h, hipStream_t s) {
+    if (!h->spin_wait) return hipStreamSynchronize(s);
+    const hipError_t e = hipEventRecord(h->ev_wait, s);
+    return e != hipSuccess ? e : host_wait(h, h->ev_wait);
+}
+
 int sync_and_verify(uno_kkt_t h) {
-    HIPCHK(h, hipEventSynchronize(h->ev_counters));  // the counters (and the dataflow abort word) are on the host
+    HIPCHK(h, host_wait(h, h->ev_counters));  // the counters (and the dataflow abort word) are on the host
     uint32_t ab = 0;
     memcpy(&ab, h->h_counters + 11, sizeof(ab));
     if (ab != 0) {
@@ -1133,6 +1154,7 @@ int upload_structure(uno_kkt_t h) {
         if (n > 0) HIPCHK(h, hipMemsetAsync(h->scale.p, 0, sizeof(double) * n, s));  // rows of other ranks: x = 0
         HIPCHK(h, h->rowsum.alloc(n));
         HIPCHK(h, h->rmax.alloc(n));
+        h->rmax_clean = false;
         HIPCHK(h, h->w.alloc(n));
         HIPCHK(h, h->bvec.alloc(n));
         HIPCHK(h, h->xtmp.alloc(n));
@@ -1235,6 +1257,7 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.scale_in = h->w.p;      // (free until the solve)
         h->scan = SA;
         h->norm_valid = false;
+        if (!h->use_front_sweeps) h->rmax_clean = false;  // the paths below use rmax as scratch
         if (h->use_front_sweeps) {
             SweepArgs W;
             W.nf = S.nf; W.n = S.n; W.fm = h->fm.p; W.rows_off = h->rows_off.p; W.rows = h->rows.p;
@@ -1248,7 +1271,9 @@ int enqueue_factorization(uno_kkt_t h) {
             W.coalesced = h->sweep_coalesced;
             W.rows_total = (int64_t)S.rows.size();
             W.flong = h->n_long > 0 ? h->flong.p : nullptr;
+            W.rmax_zero = h->rmax_clean;
             HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
+            h->rmax_clean = true;  // the last k_sweep_update cleared it
             if (h->overlap_norm && !h->exact_next) {
                 h->last_optimistic = true;  // row sums only if a pivot is small (sync_and_verify)
             } else {
@@ -1406,6 +1431,7 @@ int uno_kkt_create(uno_kkt_t* handle, int device_id) {
         hipEventCreateWithFlags(&h->ev_scale, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_norm, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&h->ev_counters, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&h->ev_wait, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&h->h_counters, 12 * sizeof(unsigned long long)) != hipSuccess ||
         hipHostMalloc((void**)&h->h_big, sizeof(int32_t)) != hipSuccess) {
         delete h;
@@ -1443,6 +1469,7 @@ void uno_kkt_destroy(uno_kkt_t h) {
     if (h->ev_scale) hipEventDestroy(h->ev_scale);
     if (h->ev_norm) hipEventDestroy(h->ev_norm);
     if (h->ev_counters) hipEventDestroy(h->ev_counters);
+    if (h->ev_wait) hipEventDestroy(h->ev_wait);
     if (h->stream2) hipStreamDestroy(h->stream2);
     if (h->stream3) { hipStreamSynchronize(h->stream3); hipStreamDestroy(h->stream3); }
     if (h->ev_fork) hipEventDestroy(h->ev_fork);
@@ -1480,6 +1507,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "solve_stamps") h->want_solve_stamps = (int)value;
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
     else if (n == "early_xpos") h->early_xpos = value != 0.0;
+    else if (n == "spin_wait") h->spin_wait = value != 0.0;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
     else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
     else if (n == "wpe2") h->wpe2 = value != 0.0;
@@ -1841,7 +1869,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
         // one GPU: k_xs_out itself skips the write of x on an abort (x may alias the rhs); the flag is read
         // in the same call and the solve redone with the level schedule
         HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-        HIPCHK(h, hipStreamSynchronize(s));
+        HIPCHK(h, host_wait_stream(h, s));
         if (dataflow_aborted(h)) {
             if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: this solve redone level by level\n");

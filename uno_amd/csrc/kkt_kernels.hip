@@ -3704,7 +3704,7 @@ hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
     A.diag_noatomic = noatomic;
     const size_t sh = 16 * (size_t)std::max(A.max_m, 1);
     const dim3 gn(grid_for(A.n, 256));
-    hipError_t e = hipMemsetAsync(A.rmax, 0, sizeof(unsigned long long) * A.n, s);
+    hipError_t e = A.rmax_zero ? hipSuccess : hipMemsetAsync(A.rmax, 0, sizeof(unsigned long long) * A.n, s);
     if (e != hipSuccess) return e;
     if (A.nf > 0) {  // COO values -> packed slots (duplicates summed)
         e = launch_pack(A.values, A.dup_ptr, A.dup_pos, A.slot_src, 0, A.ent_total, A.uval, s);

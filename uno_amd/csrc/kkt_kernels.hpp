@@ -172,6 +172,7 @@ struct SweepArgs {
     const int8_t* flong = nullptr;  // per front row: longpos of its row (-1: not a long row); nullptr: no long rows
     const int32_t* big_list;    // fronts of more than kSweepBigSlots slots (swept by 2-D grids)
     int32_t n_big = 0, big_slices = 1;
+    int rmax_zero = 0;  // rmax is known to be all zero (k_sweep_update leaves it so): no clearing memset
 };
 hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s);
 hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
