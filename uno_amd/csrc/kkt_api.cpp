@@ -209,6 +209,7 @@ struct uno_kkt {
     hipEvent_t ev_wait = nullptr;      // host_wait_stream
     int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
     bool rmax_clean = false;           // rmax all zero (left so by the front sweeps)
+    int big_app = 1;                   // option "big_app": large fronts by a-posteriori kAppNB-column steps
     int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
                                  // factorization (1), also before every sweep (2)
     int sweep_coalesced = 1;     // option "sweep_coalesced"
@@ -340,7 +341,7 @@ int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, cons
     const int count = L.count, mmax = L.mmax;
     if (count <= 0) return UNO_KKT_OK;
     HIPCHK(h, launch_big_assemble(A, fronts, count, mmax, L.maxch, s));
-    const int nb = big_panel_width(mmax);
+    const int nb = big_panel_width(mmax, A.big_app != 0);
     // one panel step per nb pivots of the widest front (+2 for early panel stops before the first check)
     int batch = (L.pmax + nb - 1) / nb + 2;
     int64_t steps = 0;
@@ -1022,7 +1023,8 @@ int upload_structure(uno_kkt_t h) {
         if (S.f_m[f] > kMaxLdsFront) {
             gtot += 8;
             goff[f] = gtot;
-            gtot += (int64_t)S.f_m[f] * S.f_m[f];
+            // the front, then the a-posteriori step's panel (m x kAppNB) and its AppSlot
+            gtot += (int64_t)S.f_m[f] * S.f_m[f] + (int64_t)S.f_m[f] * kAppNB + kAppSlotDoubles;
         } else {
             goff[f] = gtot;
         }
@@ -1314,6 +1316,7 @@ int enqueue_factorization(uno_kkt_t h) {
     static const int diag_nopiv = getenv("UNO_KKT_DIAG_NOPIV") ? atoi(getenv("UNO_KKT_DIAG_NOPIV")) : 0;
     A.diag_nopiv = diag_nopiv;
     A.big = h->big.p;
+    A.big_app = h->big_app;
     if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     A.stamps = nullptr;
@@ -1508,6 +1511,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
     else if (n == "early_xpos") h->early_xpos = value != 0.0;
     else if (n == "spin_wait") h->spin_wait = value != 0.0;
+    else if (n == "big_app") h->big_app = value != 0.0;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
     else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
     else if (n == "wpe2") h->wpe2 = value != 0.0;

@@ -2970,6 +2970,7 @@ __global__ __launch_bounds__(kThreads) void k_big_panel(FactorArgs A, const int3
         if (tid == 0 && S.k1 != S.k0) { A.big[f].k0 = S.k1; }
         return;
     }
+    if (A.big_app && !S.exact) return;  // the a-posteriori step is in charge (k_app_*)
     const int m = A.fm[f], p = A.fp[f];
     const int64_t ro = A.rows_off[f];
     const FullStore st{A.gscratch + A.gscratch_off[f], m};
@@ -3077,6 +3078,7 @@ __global__ __launch_bounds__(kThreads) void k_big_panel(FactorArgs A, const int3
         S.k1 = k;
         S.k = k;
         S.done = k >= p;
+        S.exact = 0;
         A.big[f] = S;
     }
 }
@@ -3113,6 +3115,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         if (tid == 0 && SF.k1 != SF.k0) { A.big[f].k0 = SF.k1; }
         return;
     }
+    if (A.big_app && !SF.exact) return;  // the a-posteriori step is in charge (k_app_*)
     const int m = A.fm[f], p = A.fp[f];
     const int64_t ro = A.rows_off[f];
     const FullStore st{A.gscratch + A.gscratch_off[f], m};
@@ -3433,6 +3436,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         SF.k1 = k;
         SF.k = k;
         SF.done = k >= p;
+        SF.exact = 0;
         SF.pad = min(k0 + NB, m);  // first row / column of the trailing update (the panel is current)
         A.big[f] = SF;
     }
@@ -3499,6 +3503,245 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
     for (int c = 0; c < 4; ++c) {
         if (diag && c > w) continue;
         const int j0 = u0 + 64 * tj + 16 * c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + lk + 4 * r, j = j0 + lr;
+            if (i < m && j < m && j <= i) st.at(i, j) = acc[c][r];
+        }
+    }
+}
+
+// ---- a-posteriori blocked steps (FactorArgs::big_app) ----
+// One step takes the next kAppNB columns of every unfinished large front in three launches, so the trailing
+// matrix is read and written once per kAppNB pivots (one rank-kAppNB MFMA update) instead of once per
+// register panel of 8 or 16:
+//   k_app_diag   one wave per front: the diagonal block right-looking in registers (lane = row), each
+//                column's quick Duff-Reid 1x1 test over the block's rows; the first failure ends the block
+//                (nbt columns pass).  W (un-normalised columns) into the step's panel, pivots into AppSlot.
+//   k_app_rows   the rows below, one per lane: W(i, c) = A(i, c) - sum_{q < c} L(i, q) W(c, q), L = W / d
+//                (k_big_panel_reg's products, pivots ascending), into the panel; per-column max |W(i, c)|
+//                by atomic max of the bits.  The last block to arrive applies the complete quick test
+//                u max_i |W(i, c)| <= |d_c| a posteriori: the first failing column ends the accepted run
+//                (nacc) -- the later columns' W used a rejected pivot and are discarded (column c of W
+//                depends on pivots <= c only) -- and commits pivots, counters and the front state.
+//   k_app_update C -= L W^T of the nacc accepted pivots over the trailing lower triangle from column k0 + nacc
+//                (A / B tiles staged in LDS, v_mfma_f64_16x16x4f64), plus the accepted columns (W form,
+//                diagonal = d) copied into the front.
+// The accepted pivots are the ones the register panel's quick test would accept on the same column values
+// (up to the rounding of the MFMA update order).  A failure leaves the front current at the failing column
+// with BigFrontState::exact set: the register panel then runs its exact search there (interchanges, 2x2,
+// null pivots, relaxation, delays) and k_big_update applies its pivots, in the same step.
+__device__ __forceinline__ double* app_panel(const FactorArgs& A, int f, int m) {
+    return A.gscratch + A.gscratch_off[f] + (int64_t)m * m;
+}
+__device__ __forceinline__ AppSlot* app_slot(const FactorArgs& A, int f, int m) {
+    return reinterpret_cast<AppSlot*>(app_panel(A, f, m) + (int64_t)m * kAppNB);
+}
+
+__global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __restrict__ fronts) {
+    __shared__ double colc[kAppNB];
+    const int lane = threadIdx.x;
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    BigFrontState* Sg = A.big + f;
+    const int k = Sg->k;
+    AppSlot* sl = app_slot(A, f, m);
+    const int nb = Sg->done ? 0 : min(kAppNB, p - k);
+    if (nb <= 0) {
+        if (lane == 0) { sl->nbt = 0; sl->nacc = 0; Sg->k0 = Sg->k1; }
+        return;
+    }
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+    const double* row = st.F + (int64_t)(k + (lane < nb ? lane : 0)) * m + k;
+    double a[kAppNB];
+#pragma unroll
+    for (int c = 0; c < kAppNB; ++c) a[c] = (lane < nb && c <= lane) ? row[c] : 0.0;
+    int nbt = nb;
+#pragma unroll
+    for (int c = 0; c < kAppNB; ++c) {
+        if (c >= nbt) continue;  // uniform (no break: the loop stays unrolled, a[] in registers)
+        const double akk = __shfl(a[c], c);
+        const double g = wave_max_abs((lane > c && lane < nb) ? fabs(a[c]) : 0.0);
+        const double aak = fabs(akk);
+        if (!(aak > thres) || A.u * g > aak) { nbt = c; continue; }  // uniform
+        if (lane == 0) { sl->d[c] = akk; sl->cmax[c] = as_bits(g); }
+        const double l = lane > c ? a[c] * (1.0 / akk) : 0.0;
+        colc[lane] = a[c];  // W(k + lane, c)
+        __syncthreads();
+#pragma unroll
+        for (int j = c + 1; j < kAppNB; ++j) a[j] -= l * colc[j];
+        __syncthreads();
+    }
+    if (lane < nbt) {
+        double* pr = app_panel(A, f, m) + (int64_t)lane * kAppNB;
+#pragma unroll
+        for (int c = 0; c < kAppNB; ++c)
+            if (c <= lane) pr[c] = a[c];
+    }
+    if (lane == 0) {
+        sl->k0 = k; sl->nbt = nbt; sl->nb = nb; sl->nacc = 0; sl->arrive = 0u;
+        if (nbt == 0) Sg->exact = 1;  // the first column fails already within the block
+        Sg->k0 = Sg->k1;              // nothing pending for k_big_update unless the register panel runs
+    }
+}
+
+// quad_perm broadcast of lane s of each quad (s a constant once the caller's loop is unrolled)
+__device__ __forceinline__ double quad_bcast(double v, int s) {
+    switch (s & 3) {
+        case 0: return as_double(dpp64<0x00>(as_bits(v)));
+        case 1: return as_double(dpp64<0x55>(as_bits(v)));
+        case 2: return as_double(dpp64<0xAA>(as_bits(v)));
+        default: return as_double(dpp64<0xFF>(as_bits(v)));
+    }
+}
+
+// 64 rows per block, four lanes per row: lane q of a quad owns the row's columns q, q + 4, ... (balanced
+// over the triangle); column c's multiplier comes from its owner by a quad broadcast
+__global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* __restrict__ fronts) {
+    __shared__ __attribute__((aligned(16))) double WdS[kAppNB][4][kAppNB / 4];  // W(k0 + 4jj + q, c) at [c][q][jj]
+    __shared__ double amax[kAppNB][kAppNB + 1];                              // |W| of the block's rows, [col][row]
+    __shared__ double dinv[kAppNB];
+    __shared__ int last;
+    const int tid = threadIdx.x, q = tid & 3, rl = tid >> 2;
+    const int lane = tid & 63;
+    const int f = fronts[blockIdx.y];
+    const int m = A.fm[f];
+    AppSlot* sl = app_slot(A, f, m);
+    const int nbt = sl->nbt;
+    if (nbt == 0) return;  // no step for this front (done, or the register panel's exact search is next)
+    const int k0 = sl->k0;
+    double* P = app_panel(A, f, m);
+    for (int t = tid; t < kAppNB * kAppNB; t += 256) {
+        const int j = t >> 6, c = t & 63;
+        WdS[c][j & 3][j >> 2] = (c < j && j < nbt) ? P[(int64_t)j * kAppNB + c] : 0.0;
+    }
+    if (tid < kAppNB) dinv[tid] = tid < nbt ? 1.0 / sl->d[tid] : 0.0;
+    __syncthreads();
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const int i = k0 + nbt + (int)blockIdx.x * 64 + rl;
+    const bool valid = i < m;
+    const double* row = st.F + (int64_t)(valid ? i : k0) * m + k0;
+    double w[kAppNB / 4];
+#pragma unroll
+    for (int jj = 0; jj < kAppNB / 4; ++jj) w[jj] = (valid && 4 * jj + q < nbt) ? row[4 * jj + q] : 0.0;
+#pragma unroll
+    for (int c = 0; c < kAppNB; ++c) {
+        const double l = quad_bcast(w[c >> 2] * dinv[c], c & 3);  // 0 from column nbt on
+        const double* wd = &WdS[c][q][0];
+#pragma unroll
+        for (int jj = c >> 2; jj < kAppNB / 4; ++jj) w[jj] -= l * wd[jj];  // W(., c) = 0 at columns <= c
+    }
+    if (valid) {
+        double* pw = P + (int64_t)(i - k0) * kAppNB;
+#pragma unroll
+        for (int jj = 0; jj < kAppNB / 4; ++jj)
+            if (4 * jj + q < nbt) pw[4 * jj + q] = w[jj];
+    }
+#pragma unroll
+    for (int jj = 0; jj < kAppNB / 4; ++jj) amax[4 * jj + q][rl] = fabs(w[jj]);  // invalid rows hold 0
+    __syncthreads();
+    if (tid < kAppNB) {
+        double g = 0.0;
+        for (int r = 0; r < 64; ++r) g = fmax(g, amax[tid][r]);
+        if (tid < nbt && g > 0.0) atomicMax(&sl->cmax[tid], as_bits(g));
+    }
+    __threadfence();
+    __syncthreads();
+    if (tid == 0) last = atomicAdd(&sl->arrive, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last || tid >= 64) return;
+    __threadfence();
+    // every block's maxima are in: the a-posteriori test and the commit
+    const unsigned long long cm = lane < nbt ? __hip_atomic_load(&sl->cmax[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+    const double dd = lane < nbt ? sl->d[lane] : 0.0;
+    const unsigned long long bad = __ballot(lane < nbt && A.u * as_double(cm) > fabs(dd));
+    const int nacc = bad ? (int)__builtin_ctzll(bad) : nbt;
+    const bool acc = lane < nacc;
+    if (acc) A.piv[A.rows_off[f] + k0 + lane] = PIV_1X1;
+    const int npos = (int)__popcll(__ballot(acc && dd > 0.0));
+    double mn = acc ? fabs(dd) : INFINITY;
+    for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
+    if (lane == 0) {
+        BigFrontState S = A.big[f];
+        S.npos += npos;
+        S.nneg += nacc - npos;
+        S.minpiv = fmin(S.minpiv, mn);
+        S.k = k0 + nacc;
+        S.k0 = S.k;
+        S.k1 = S.k;
+        S.done = S.k >= A.fp[f];
+        S.exact = (!S.done && nacc < sl->nb) ? 1 : 0;
+        A.big[f] = S;
+        sl->nacc = nacc;
+    }
+}
+
+// grid.x: tiles_max trailing tiles (lower-triangular order, 64 x 64, wave w owns rows 16w..16w+15 as in
+// k_big_update), then ceil(mmax / 64) copy blocks of 64 panel rows each
+__global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int32_t* __restrict__ fronts, int tiles_max) {
+    __shared__ __attribute__((aligned(16))) double As[kAppNB][64 + 2];  // -L(i0t + r, q) at [q][r]
+    __shared__ __attribute__((aligned(16))) double Bs[kAppNB][64 + 2];  //  W(j0t + c, q) at [q][c]
+    __shared__ double dinv[kAppNB];
+    const int f = fronts[blockIdx.y];
+    const int m = A.fm[f];
+    const AppSlot* sl = app_slot(A, f, m);
+    const int nacc = sl->nacc;
+    if (nacc == 0) return;
+    const int k0 = sl->k0, u0 = k0 + nacc;
+    const double* P = app_panel(A, f, m);
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    const int tid = threadIdx.x;
+    if ((int)blockIdx.x >= tiles_max) {  // the accepted columns into the front
+        const int rb = (int)blockIdx.x - tiles_max;
+        for (int t = tid; t < 64 * kAppNB; t += kThreads) {
+            const int rr = 64 * rb + (t >> 6), q = t & 63;
+            const int i = k0 + rr;
+            if (i < m && q < nacc && q <= rr) st.at(i, k0 + q) = P[(int64_t)rr * kAppNB + q];
+        }
+        return;
+    }
+    const int nt = (m - u0 + 63) / 64;
+    if ((int)blockIdx.x >= nt * (nt + 1) / 2) return;
+    int ti, tj;
+    tri_rc((int)blockIdx.x, ti, tj);
+    const int i0t = u0 + 64 * ti, j0t = u0 + 64 * tj;
+    if (tid < kAppNB) dinv[tid] = tid < nacc ? 1.0 / sl->d[tid] : 0.0;
+    __syncthreads();
+    for (int t = tid; t < 64 * kAppNB; t += kThreads) {
+        const int r = t >> 6, q = t & 63;
+        const int i = i0t + r, j = j0t + r;
+        As[q][r] = (i < m && q < nacc) ? -(P[(int64_t)(i - k0) * kAppNB + q] * dinv[q]) : 0.0;
+        Bs[q][r] = (j < m && q < nacc) ? P[(int64_t)(j - k0) * kAppNB + q] : 0.0;
+    }
+    const int lane = tid & 63, w = tid >> 6;
+    const int lr = lane & 15, lk = lane >> 4;
+    const int i0 = i0t + 16 * w;
+    dbl4 acc[4];
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int j0 = j0t + 16 * c;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+            const int i = i0 + lk + 4 * r, j = j0 + lr;
+            acc[c][r] = (i < m && j < m && j <= i) ? st.at(i, j) : 0.0;
+        }
+    }
+    __syncthreads();
+    const bool diag = ti == tj;
+    for (int q = 0; q < nacc; q += 4) {
+        const double a = As[q + lk][16 * w + lr];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (diag && c > w) continue;  // wave-uniform: strip entirely above the diagonal
+            const double b = Bs[q + lk][16 * c + lr];
+            acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        if (diag && c > w) continue;
+        const int j0 = j0t + 16 * c;
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
             const int i = i0 + lk + 4 * r, j = j0 + lr;
@@ -3936,6 +4179,12 @@ hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int c
 
 hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
     if (count <= 0) return hipSuccess;
+    if (A.big_app) {
+        const int rb = (mmax + 63) / 64;
+        hipLaunchKernelGGL(k_app_diag, dim3(count), dim3(64), 0, s, A, fronts);
+        hipLaunchKernelGGL(k_app_rows, dim3(rb, count), dim3(256), 0, s, A, fronts);
+        hipLaunchKernelGGL(k_app_update, dim3(rb * (rb + 1) / 2 + rb, count), dim3(kThreads), 0, s, A, fronts, rb * (rb + 1) / 2);
+    }
     static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;  // diagnostics: the left-looking panel
     if (legacy || mmax > 16 * kThreads) hipLaunchKernelGGL(k_big_panel, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(double) + 16, s, A, fronts);
     else if (mmax <= 256) hipLaunchKernelGGL((k_big_panel_reg<1, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
@@ -3959,7 +4208,8 @@ hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int cou
     return hipGetLastError();
 }
 
-int big_panel_width(int mmax) {
+int big_panel_width(int mmax, bool app) {
+    if (app) return kAppNB;
     static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;
     return (legacy || mmax > 16 * kThreads) ? kBigNB : (mmax > 1024 ? 8 : 16);
 }

@@ -13,8 +13,23 @@ struct BigFrontState {
     int32_t k0, k1;     // pivots of the last panel: [k0, k1) (its trailing update is applied by k_big_update)
     int32_t done;
     int32_t npos, nneg, nzero, n2, nrel, nstuck, delays, pad;
+    int32_t exact;      // a-posteriori step (FactorArgs::big_app) stopped at a failing column: the register
+                        // panel's exact search runs next (k_big_panel_reg / k_big_panel), then clears it
     double minpiv;      // smallest pivot magnitude accepted as non-null
 };
+
+// a-posteriori blocked steps of the large fronts (k_app_*): kAppNB columns per step; per big front the
+// global scratch holds, after its m x m front, the step's panel (m x kAppNB, row-major) and an AppSlot
+constexpr int kAppNB = 64;
+struct AppSlot {
+    unsigned long long cmax[kAppNB];  // max |W(i, c)| over the rows below the diagonal (bits; atomic max)
+    double d[kAppNB];                 // the diagonal block's pivots
+    int32_t k0, nbt, nacc, nb;        // first column, columns passing the in-block test, accepted, block width
+    uint32_t arrive;                  // k_app_rows blocks done (the last one decides nacc)
+    int32_t pad_[3];
+};
+constexpr int64_t kAppSlotDoubles = 160;
+static_assert(sizeof(AppSlot) <= kAppSlotDoubles * sizeof(double), "AppSlot");
 
 // Arguments of the front factorization kernels (device pointers, SoA per front).
 struct FactorArgs {
@@ -67,6 +82,7 @@ struct FactorArgs {
     uint32_t* df_ticket;        // block start order (cumulative: (epoch - 1) * df_nf at launch)
     uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
     BigFrontState* big;         // per front: state of the blocked large-front factorization (m > kMaxLdsFront)
+    int big_app;                // 1: a-posteriori kAppNB-column steps with one rank-kAppNB MFMA update (k_app_*)
 };
 
 struct SolveArgs {
@@ -245,7 +261,7 @@ hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int c
 hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
 hipError_t launch_big_pending(const FactorArgs& A, const int32_t* fronts, int count, int32_t* out, hipStream_t s);
 hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
-int big_panel_width(int mmax);  // pivots per panel step of the large-front launches
+int big_panel_width(int mmax, bool app);  // pivots per panel step of the large-front launches
 
 // dataflow factorization of the upper tree (one-wave fronts, m <= 64)
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
