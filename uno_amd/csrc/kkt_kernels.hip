@@ -695,6 +695,8 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x)
 // non-negative doubles compare like their bit patterns
 __device__ __forceinline__ double wave_max_abs(double v) { return as_double(wave_max_u64(as_bits(v))); }
 
+template <class S> constexpr bool kFullStore = std::is_same<S, FullStore>::value;
+
 // Threshold pivot search (MUMPS/Duff-Reid rule, u then relaxed); run by one full wave, result
 // wave-uniform.  Mirrors test_pivot() of oracle/kkt_oracle.c; the relaxed ladder is only used at
 // roots or when delays are disabled (otherwise the first relaxation reports the delayed columns).
@@ -707,9 +709,16 @@ __device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u
         const double uu = ul == 0 ? u : ul == 1 ? u * 0.1 : ul == 2 ? u * 0.01 : ul == 3 ? 1e-6 : ul == 4 ? 1e-10 : 0.0;
         for (int c = k; c < p; ++c) {
             double g = 0.0;
-            for (int i = k + lane; i < m; i += 64) {
-                if (i == c) continue;
-                g = fmax(g, absA(st, i, c));
+            if constexpr (kFullStore<S>) {
+                // front in HBM (large fronts): eight rows in flight per lane instead of one dependent load
+                // after the other (~0.3 us each at m = 4096)
+#pragma unroll 8
+                for (int i = k + lane; i < m; i += 64) g = fmax(g, i == c ? 0.0 : absA(st, i, c));
+            } else {
+                for (int i = k + lane; i < m; i += 64) {
+                    if (i == c) continue;
+                    g = fmax(g, absA(st, i, c));
+                }
             }
             g = wave_max_abs(g);
             const double acc = fabs(st.at(c, c));
@@ -720,20 +729,37 @@ __device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u
             // exact argmax, ties to the smallest row (oracle test_pivot: first strict maximum)
             unsigned long long best = 0;
             int bi = 0x7fffffff;
-            for (int i = k + lane; i < p; i += 64) {
-                if (i == c) continue;
-                const unsigned long long b = as_bits(absA(st, i, c));
-                if (b > best) { best = b; bi = i; }  // rows ascending per lane: a tie keeps the smaller row
+            if constexpr (kFullStore<S>) {
+#pragma unroll 8
+                for (int i = k + lane; i < p; i += 64) {
+                    const unsigned long long b = i == c ? 0ull : as_bits(absA(st, i, c));
+                    if (b > best) { best = b; bi = i; }  // rows ascending per lane: a tie keeps the smaller row
+                }
+            } else {
+                for (int i = k + lane; i < p; i += 64) {
+                    if (i == c) continue;
+                    const unsigned long long b = as_bits(absA(st, i, c));
+                    if (b > best) { best = b; bi = i; }  // rows ascending per lane: a tie keeps the smaller row
+                }
             }
             const unsigned long long mx = wave_max_u64(best);
             const unsigned long long ik = wave_max_u64(mx != 0 && best == mx ? 0xffffffffull - (unsigned)bi : 0ull);
             if (mx != 0) {
                 const int r = (int)(0xffffffffull - ik);
                 double gc = 0.0, gr = 0.0;
-                for (int i = k + lane; i < m; i += 64) {
-                    if (i == c || i == r) continue;
-                    gc = fmax(gc, absA(st, i, c));
-                    gr = fmax(gr, absA(st, i, r));
+                if constexpr (kFullStore<S>) {
+#pragma unroll 8
+                    for (int i = k + lane; i < m; i += 64) {
+                        const bool skip = i == c || i == r;
+                        gc = fmax(gc, skip ? 0.0 : absA(st, i, c));
+                        gr = fmax(gr, skip ? 0.0 : absA(st, i, r));
+                    }
+                } else {
+                    for (int i = k + lane; i < m; i += 64) {
+                        if (i == c || i == r) continue;
+                        gc = fmax(gc, absA(st, i, c));
+                        gr = fmax(gr, absA(st, i, r));
+                    }
                 }
                 gc = wave_max_abs(gc);
                 gr = wave_max_abs(gr);
@@ -752,6 +778,101 @@ __device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u
         }
     }
     return d;
+}
+
+// search_pivot for the large fronts in HBM (k_big_panel_reg): the same rule and the same decisions, every
+// thread of the block scanning rows (the one-wave scans cost ~15 us per column at m = 4096)
+template <int T>
+__device__ PivotDecision search_pivot_blk(const FullStore& st, int m, int k, int p, double u, double thres,
+                                          double& minpiv, unsigned long long* red) {
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    auto bmax = [&](unsigned long long v) __attribute__((always_inline)) -> unsigned long long {
+        v = wave_max_u64(v);
+        if (lane == 0) red[wv] = v;
+        __syncthreads();
+        unsigned long long r = red[0];
+#pragma unroll
+        for (int w = 1; w < T / 64; ++w) r = umax64(r, red[w]);
+        __syncthreads();
+        return r;
+    };
+    PivotDecision d{PIV_STUCK, k, -1, 0};
+    for (int ul = 0; ul < 6; ++ul) {
+        const double uu = ul == 0 ? u : ul == 1 ? u * 0.1 : ul == 2 ? u * 0.01 : ul == 3 ? 1e-6 : ul == 4 ? 1e-10 : 0.0;
+        for (int c = k; c < p; ++c) {
+            double g = 0.0;
+#pragma unroll 4
+            for (int i = k + tid; i < m; i += T) g = fmax(g, i == c ? 0.0 : absA(st, i, c));
+            g = as_double(bmax(as_bits(g)));
+            const double acc = fabs(st.at(c, c));
+            if (fmax(acc, g) <= thres) { d.kind = PIV_NULL; d.c = c; d.relaxed = ul > 0; return d; }
+            minpiv = fmin(minpiv, fmax(acc, g));
+            if (acc != 0.0 && acc >= uu * g) { d.kind = PIV_1X1; d.c = c; d.relaxed = ul > 0; return d; }
+            unsigned long long best = 0;
+            int bi = 0x7fffffff;
+#pragma unroll 4
+            for (int i = k + tid; i < p; i += T) {
+                const unsigned long long b = i == c ? 0ull : as_bits(absA(st, i, c));
+                if (b > best) { best = b; bi = i; }  // rows ascending per thread: a tie keeps the smaller row
+            }
+            const unsigned long long mx = bmax(best);
+            const unsigned long long ik = bmax(mx != 0 && best == mx ? 0xffffffffull - (unsigned)bi : 0ull);
+            if (mx != 0) {
+                const int r = (int)(0xffffffffull - ik);
+                double gc = 0.0, gr = 0.0;
+#pragma unroll 4
+                for (int i = k + tid; i < m; i += T) {
+                    const bool skip = i == c || i == r;
+                    gc = fmax(gc, skip ? 0.0 : absA(st, i, c));
+                    gr = fmax(gr, skip ? 0.0 : absA(st, i, r));
+                }
+                gc = as_double(bmax(as_bits(gc)));
+                gr = as_double(bmax(as_bits(gr)));
+                const double a = st.at(c, c);
+                const double b = r > c ? st.at(r, c) : st.at(c, r);
+                const double e = st.at(r, r);
+                const double det = a * e - b * b;
+                if (det != 0.0) {
+                    const double lim = uu > 0.0 ? fabs(det) / uu : INFINITY;
+                    if (fabs(e) * gc + fabs(b) * gr <= lim && fabs(b) * gc + fabs(a) * gr <= lim) {
+                        d.kind = PIV_2X2_A; d.c = c; d.r = r; d.relaxed = ul > 0;
+                        return d;
+                    }
+                }
+            }
+        }
+    }
+    return d;
+}
+
+// sym_swap for a front in HBM: eight positions per thread loaded before any is stored (the positions are
+// distinct), instead of one dependent load/store round trip after the other
+template <int NT>
+__device__ void sym_swap_batched(const FullStore& st, int m, int a, int b, int32_t* lrow, int32_t* lorig) {
+    for (int t0 = threadIdx.x; t0 < m; t0 += 8 * NT) {
+        int p1[8], p2[8];
+        double v1[8], v2[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+            const int t = t0 + q * NT;
+            p1[q] = -1; p2[q] = -1;
+            if (t >= m || t == b) continue;
+            if (t < a) { p1[q] = st.idx(a, t); p2[q] = st.idx(b, t); }
+            else if (t == a) { p1[q] = st.idx(a, a); p2[q] = st.idx(b, b); }
+            else if (t < b) { p1[q] = st.idx(t, a); p2[q] = st.idx(b, t); }
+            else { p1[q] = st.idx(t, a); p2[q] = st.idx(t, b); }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (p1[q] >= 0) { v1[q] = st.F[p1[q]]; v2[q] = st.F[p2[q]]; }
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+            if (p1[q] >= 0) { st.F[p1[q]] = v2[q]; st.F[p2[q]] = v1[q]; }
+    }
+    if (threadIdx.x == 0) {
+        int32_t y = lrow[a]; lrow[a] = lrow[b]; lrow[b] = y;
+        y = lorig[a]; lorig[a] = lorig[b]; lorig[b] = y;
+    }
 }
 
 // Fast path of the same rule for the first candidate (c = k): every lane tests its own entries
@@ -3126,6 +3247,16 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
     double minpiv = SF.minpiv;  // uniform
     const int k0 = SF.k;
     const int ncol = min(NB, p - k0);  // fully-summed columns of this panel
+    // diagnostics (option stamps = 6): s_memrealtime ticks per phase summed into stamps[8 f + phase]
+    const bool stamp = A.stamps != nullptr && A.stamp_mode == 6 && tid == 0;
+    unsigned long long t_last = stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
+    auto tick = [&](int ph) __attribute__((always_inline)) {
+        if (stamp) {
+            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+            atomicAdd(&A.stamps[8 * (int64_t)f + ph], t - t_last);
+            t_last = t;
+        }
+    };
     // one vector register tuple per owned row: static columns in the pivot steps, dynamic (uniform) ones in
     // the in-panel search via indexed register moves -- never scratch
     typedef double RowV __attribute__((ext_vector_type(NB)));
@@ -3187,6 +3318,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
     bool full = false;
     if (ncol > 0) {
         double g0 = 0.0;
+#pragma unroll 8
         for (int i = k0 + 1 + tid; i < m; i += T) g0 = fmax(g0, fabs(st.at(i, k0)));
         g0 = wave_max_abs(g0);
         if (lane == 0) red[0][wv] = g0;
@@ -3200,21 +3332,21 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
     }
     if (full) {
         const int k = k0;
-        if (tid < 64) {
-            const PivotDecision d = search_pivot(st, m, k, p, A.u, thres, minpiv);
+        {
+            const PivotDecision d = search_pivot_blk<T>(st, m, k, p, A.u, thres, minpiv, ured);
             if (tid == 0) sh.dec = d;
         }
         __syncthreads();
         PivotDecision d = sh.dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
-            sym_swap<T>(st, m, k, d.c, lrow, lorig);
+            sym_swap_batched<T>(st, m, k, d.c, lrow, lorig);
             __syncthreads();
         }
         if (d.kind == PIV_2X2_A) {
             const int r = d.r == k ? d.c : d.r;
             if (r != k + 1) {
-                sym_swap<T>(st, m, k + 1, r, lrow, lorig);
+                sym_swap_batched<T>(st, m, k + 1, r, lrow, lorig);
                 __syncthreads();
             }
         }
@@ -3254,6 +3386,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         }
         __syncthreads();
     }
+    tick(0);  // quick test of the first column (+ exact search, interchanges)
     load();
     // the interchanged front minus the exact-search pivots' terms on the panel's later columns
     for (int q = 0; q < np; ++q) {
@@ -3407,6 +3540,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         }
         return false;
     };
+    tick(1);  // register panel loaded, exact pivots' terms applied
     int cend = np;
     for (;;) {  // one call site each: the panel stays in registers
         cend = steps(cend);
@@ -3416,6 +3550,7 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
             break;
         }
     }
+    tick(2);  // quick steps
     // the panel back to the front (lower part, un-normalised): pivoted columns and the panel's later
     // columns (current: the trailing update starts after the panel, at k0 + NB)
 #pragma unroll
@@ -3440,6 +3575,8 @@ __global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 
         SF.pad = min(k0 + NB, m);  // first row / column of the trailing update (the panel is current)
         A.big[f] = SF;
     }
+    tick(3);  // write-back
+    if (stamp) atomicAdd(&A.stamps[8 * (int64_t)f + 4], 1ull);
 }
 
 // Trailing update of the pending panel [k0, k1): rows / columns [k1, m), lower triangle.  Block = one
