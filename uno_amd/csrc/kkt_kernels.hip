@@ -3814,6 +3814,84 @@ __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* _
     }
 }
 
+// The exact step of the a-posteriori path at a failing column (BigFrontState::exact): the exact search
+// (search_pivot_blk: interchanges, 2x2, null pivots, relaxation ladder, delays) decides one or two pivots
+// on the current front; their columns are already their W columns, so nothing else is computed here --
+// k_big_update applies them to the trailing matrix and the next a-posteriori step continues after them.
+// (The register panel k_big_panel_reg would also load and write back NB columns: ~35 us more per step
+// at m = 4096.)
+__global__ __launch_bounds__(512) void k_app_exact(FactorArgs A, const int32_t* __restrict__ fronts) {
+    constexpr int T = 512;
+    __shared__ unsigned long long ured[T / 64];
+    __shared__ BigFrontState SF;
+    const int tid = threadIdx.x;
+    const int f = fronts[blockIdx.x];
+    if (tid == 0) SF = A.big[f];
+    __syncthreads();
+    if (SF.done || !SF.exact) return;
+    const int m = A.fm[f], p = A.fp[f];
+    const int64_t ro = A.rows_off[f];
+    const FullStore st{A.gscratch + A.gscratch_off[f], m};
+    int32_t* lrow = A.frow + ro;
+    int32_t* lorig = A.fpos + ro;
+    int8_t* piv = A.piv + ro;
+    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+    double minpiv = SF.minpiv;
+    const int k = SF.k;
+    PivotDecision d = search_pivot_blk<T>(st, m, k, p, A.u, thres, minpiv, ured);
+    const bool stuck = d.kind == PIV_STUCK;
+    if (stuck) { d.kind = PIV_NULL; d.c = k; }
+    if (d.c != k) {
+        sym_swap_batched<T>(st, m, k, d.c, lrow, lorig);
+        __syncthreads();
+    }
+    if (d.kind == PIV_2X2_A) {
+        const int r = d.r == k ? d.c : d.r;
+        if (r != k + 1) {
+            sym_swap_batched<T>(st, m, k + 1, r, lrow, lorig);
+            __syncthreads();
+        }
+    }
+    int np = 1;
+    if (d.kind == PIV_NULL) {
+        for (int i = k + 1 + tid; i < m; i += T) st.at(i, k) = 0.0;
+    } else if (d.kind == PIV_2X2_A) {
+        np = 2;
+    }
+    if (tid == 0) {
+        if (stuck) SF.nstuck++;
+        SF.nrel += d.relaxed;
+        if (d.relaxed && !SF.delays && A.record_delays && A.fparent[f] >= 0) {  // see factor_front
+            SF.delays = 1;
+            const unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
+            for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
+        }
+        if (d.kind == PIV_NULL) {
+            piv[k] = PIV_NULL;
+            SF.nzero++;
+        } else if (d.kind == PIV_1X1) {
+            const double dk = st.at(k, k);
+            piv[k] = PIV_1X1;
+            if (dk > 0.0) SF.npos++; else SF.nneg++;
+        } else {
+            const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
+            const double det = a * e - b * b;
+            piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; SF.n2++;
+            if (det < 0.0) { SF.npos++; SF.nneg++; }
+            else if (a + e > 0.0) SF.npos += 2;
+            else SF.nneg += 2;
+        }
+        SF.minpiv = minpiv;
+        SF.k0 = k;
+        SF.k1 = k + np;
+        SF.k = k + np;
+        SF.pad = k + np;  // the trailing update starts right after the pivots
+        SF.done = SF.k >= p;
+        SF.exact = 0;
+        A.big[f] = SF;
+    }
+}
+
 // grid.x: tiles_max trailing tiles (lower-triangular order, 64 x 64, wave w owns rows 16w..16w+15 as in
 // k_big_update), then ceil(mmax / 64) copy blocks of 64 panel rows each
 __global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int32_t* __restrict__ fronts, int tiles_max) {
@@ -4321,6 +4399,13 @@ hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count
         hipLaunchKernelGGL(k_app_diag, dim3(count), dim3(64), 0, s, A, fronts);
         hipLaunchKernelGGL(k_app_rows, dim3(rb, count), dim3(256), 0, s, A, fronts);
         hipLaunchKernelGGL(k_app_update, dim3(rb * (rb + 1) / 2 + rb, count), dim3(kThreads), 0, s, A, fronts, rb * (rb + 1) / 2);
+        static const bool panel_exact = getenv("UNO_KKT_APP_PANEL") != nullptr;  // A/B: the register panel instead
+        if (!panel_exact) {
+            hipLaunchKernelGGL(k_app_exact, dim3(count), dim3(512), 0, s, A, fronts);
+            const int nt = (mmax + 63) / 64;
+            hipLaunchKernelGGL(k_big_update, dim3(nt * (nt + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
+            return hipGetLastError();
+        }
     }
     static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;  // diagnostics: the left-looking panel
     if (legacy || mmax > 16 * kThreads) hipLaunchKernelGGL(k_big_panel, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(double) + 16, s, A, fronts);
