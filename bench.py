@@ -403,14 +403,22 @@ def main():
                     "algorithmic": f"{bytes_solve:.4e} B per solve", "ms_per_launch_group": round(sol_ms, 4)}
         roof["kernel_ms_per_step"] = {k: round(v, 4) for k, v in others.items()}
         roof["solve_GBs"] = round(bytes_solve / (sol_ms * 1e-3) / 1e9, 2) if sol_ms > 0 else None
+        # PMC-measured HBM bytes (profiles/pmc_traffic.json, rocprofv3 FETCH_SIZE / WRITE_SIZE passes of this
+        # bench): used only when the profile was taken on this workload (same n, nnz, default analysis options)
         pmc = os.path.join(ROOT, "profiles", "pmc_traffic.json")
         pmcd = {}
         if os.path.exists(pmc):
             try:
-                pmcd = json.load(open(pmc))
-                roof["traffic"] = pmcd.get("factor_bytes_per_factorization")
+                cand = json.load(open(pmc))
+                wl = cand.get("workload", {})
+                if (wl.get("n") == n and wl.get("nnz") == len(vals) and not args.leaf and not args.block
+                        and not args.opt and world == 1):
+                    pmcd = cand
             except Exception:
-                pass
+                pmcd = {}
+        roof["traffic"] = pmcd.get("factor_bytes_per_factorization")
+        roof["traffic_source"] = (pmcd.get("source") if pmcd else
+                                  "null: profiles/pmc_traffic.json was not measured on this workload / options")
         # the triangular solve against the HBM roofline (north_star target: >= 60 %)
         if sol_ms > 0:
             sach = bytes_solve / (sol_ms * 1e-3) / 1e9
@@ -461,13 +469,17 @@ def main():
         except Exception:  # noqa: BLE001 -- informational
             affinity = None
         cpu = {"value": round(1.0 / float(np.median(per)), 4), "unit": "factor+solve/s", "cores": threads(),
+               "reps_min_max_per_s": [round(1.0 / max(per), 4), round(1.0 / min(per), 4)],
+               "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS"),
                "kind": "port",
                "sample": f"oracle/cpu_mf.cpp (multi-threaded multifrontal restatement on the product's ND analysis; "
                          f"MUMPS unavailable) on arrowband n={cn} nnz={len(cv)}: median of {reps} "
                          f"factor+inertia+solve reps ({t_cpu:.1f} s), {threads()} OpenMP threads",
                "nproc": os.cpu_count(), "affinity_cpus": affinity,
-               "cores_note": "OpenMP threads = OMP_NUM_THREADS, the CPU share the GPU lease grants per GPU "
-                             "(16 on the box; nproc / affinity show the whole host)",
+               "cores_note": "OpenMP threads = OMP_NUM_THREADS, the host-core share the GPU pool leases per GPU: the "
+                             "harness exports OMP_NUM_THREADS=16 on every 1-GPU box and caps worker pools at 16; nproc / "
+                             "sched_getaffinity show the whole shared host (other leases run on the same cores), so "
+                             "running at affinity_cpus threads would time contention, not MUMPS-class host throughput",
                "cpu_model": model,
                "inertia": list(o_inertia), "inertia_checked_against_gpu": cn == n,
                "gpu_over_cpu": round(value / (1.0 / float(np.median(per))), 1) if per else None}

@@ -27,6 +27,9 @@ int64_t uno_kkt_debug_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap, int32
 /* Option "solve_stamps" = 1: per front 8 words of the last dataflow solve, s_memrealtime (100 MHz) at
  * {start, dependency satisfied, values staged, published} of the forward (0..3) and backward (4..7) pass. */
 int64_t uno_kkt_debug_solve_stamps(uno_kkt_t handle, uint64_t* out, int64_t cap);
+/* The handle's current front structure (after any delay merges): per front order, pivots and level. */
+int64_t uno_kkt_debug_front_info(uno_kkt_t handle, int32_t* front_order, int32_t* front_pivots, int32_t* front_level,
+                                 int64_t cap);
 /* Equilibration of the last factorization: the scaling s (by original index) and ||A_pre||_inf as the
  * library computed them (waits for the factorization).  Returns 0, or an error code. */
 int uno_kkt_debug_scaling(uno_kkt_t handle, double* scale, double* anorm);

@@ -112,3 +112,138 @@ def test_big_front_refactorization_and_retry():
         b = rng.standard_normal(n)
         x = g.solve(b)
         assert np.abs((S + shift * np.eye(n)) @ x - b).max() < 1e-8 * np.abs(x).max()
+
+
+def check_eig(n, r, c, v, S, rng, zero_tol=1e-9, **opt):
+    """Inertia against numpy's eigenvalues only (orders where the one-thread oracle would take minutes):
+    eigenvalues within zero_tol * ||S||_2 of 0 count as zero; residual bar as check()."""
+    import uno_amd
+    uno_amd.load_library()
+    ev = np.linalg.eigvalsh(S)
+    tol = zero_tol * np.abs(ev).max()
+    expect = (int((ev > tol).sum()), int((ev < -tol).sum()), int((np.abs(ev) <= tol).sum()))
+    g = uno_amd.HipKKT(0, **opt)
+    g.analyze(n, r, c)
+    g.factorize(v)
+    assert g.inertia() == expect
+    if expect[2] == 0:
+        b = rng.standard_normal(n)
+        x = g.solve(b)
+        cond = np.abs(ev).max() / np.abs(ev).min()
+        assert np.abs(S @ x - b).max() <= 1e-13 * cond * np.abs(b).max() * n ** 0.5
+    return g.stats()
+
+
+def test_dense_indefinite_2048():
+    """One dense front of order 2048 through the a-posteriori 64-column steps (k_app_*) and the MFMA
+    trailing updates: inertia equal to numpy's eigenvalue count, residual bar."""
+    n = 2048
+    rng = np.random.default_rng(n)
+    A = rng.standard_normal((n, n))
+    S = (A + A.T) / 2 + np.diag(rng.uniform(-3, 3, n))
+    r, c, v = dense_coo(S)
+    st = check_eig(n, r, c, v, S, rng)
+    assert st["max_front"] == n
+
+
+def test_dense_kkt_2048():
+    """Dense saddle point of order 2048 ([[H, J^T], [J, 0]], constraints first): exact steps with 2x2 pivots
+    and interchanges all the way through the large-front path."""
+    nv, m = 1200, 848
+    rng = np.random.default_rng(nv + m)
+    H = rng.standard_normal((nv, nv)) * 0.1
+    H = H + H.T + np.diag(rng.uniform(0.5, 2.0, nv))
+    J = rng.standard_normal((m, nv))
+    S = np.block([[H, J.T], [J, np.zeros((m, m))]])
+    P = np.concatenate([np.arange(nv, nv + m), np.arange(nv)])
+    S = S[np.ix_(P, P)]
+    n = nv + m
+    r, c, v = dense_coo(S)
+    r = np.concatenate([r, np.arange(m)])
+    c = np.concatenate([c, np.arange(m)])
+    v = np.concatenate([v, np.zeros(m)])
+    st = check_eig(n, r, c, v, S, rng)
+    assert st["pivots_2x2"] > 0 and st["max_front"] == n
+
+
+@pytest.mark.parametrize("n", [200, 700])
+def test_singular_dense_front(n):
+    """Rank-deficient dense front (m > 128) through k_app_exact's null-pivot path: k rows / columns that are
+    exactly zero (explicit zeros in the pattern) and d rows duplicating other rows exactly (their pivot
+    becomes an exact 0 after the original's elimination).  Inertia (pos, neg, zero) equal to the oracle's
+    (MUMPS semantics: |pivot| <= eps * 1e-5 * ||A_pre|| is null) and to numpy's eigenvalue count."""
+    rng = np.random.default_rng(100 + n)
+    A = rng.standard_normal((n, n))
+    S = (A + A.T) / 2 + np.diag(rng.uniform(-3, 3, n))
+    zero_rows = rng.choice(n, size=5, replace=False)
+    S[zero_rows, :] = 0.0
+    S[:, zero_rows] = 0.0
+    rest = np.setdiff1d(np.arange(n), zero_rows)
+    src = rng.choice(rest, size=3, replace=False)
+    dst = rng.choice(np.setdiff1d(rest, src), size=3, replace=False)
+    for s_, d_ in zip(src, dst):  # row / column d_ := row / column s_ (symmetric duplicate)
+        S[d_, :] = S[s_, :]
+        S[:, d_] = S[:, s_]
+        S[d_, d_] = S[s_, s_]
+    rr, cc = np.tril_indices(n)
+    v = S[rr, cc]
+    import uno_amd
+    uno_amd.load_library()
+    g = uno_amd.HipKKT(0)
+    g.analyze(n, rr, cc)
+    g.factorize(v)
+    o = OracleKKT()
+    o.analyze(n, rr, cc)
+    o.factorize(v)
+    ev = np.linalg.eigvalsh(S)
+    tol = 1e-10 * np.abs(ev).max()
+    expect = (int((ev > tol).sum()), int((ev < -tol).sum()), int((np.abs(ev) <= tol).sum()))
+    assert expect[2] == 8
+    assert g.inertia() == o.inertia() == expect
+    assert g.stats()["max_front"] == n
+
+
+def test_large_front_delays_to_parent():
+    """A non-root large front whose fully-summed block cannot be pivoted inside it: a 240-row clique
+    [[H, 0], [0, 0]] whose last 60 rows couple only to 150 dense (arrow) rows that are ordered last.  With
+    MUMPS semantics (delay_relaxed = 1) the 60 columns are delayed to the root front (merge rounds), the
+    inertia equals the oracle's and numpy's and the solve meets the residual bar."""
+    rng = np.random.default_rng(23)
+    nb, na, nz, k = 4000, 180, 60, 150
+    n = nb + na + nz + k
+    S = np.zeros((n, n))
+    for d in range(4):  # banded part
+        vals = rng.standard_normal(nb - d) * (0.3 if d else 1.0)
+        S[np.arange(d, nb), np.arange(nb - d)] = vals
+    S[:nb, :nb] += np.diag(rng.uniform(1.0, 3.0, nb))
+    H = rng.standard_normal((na, na))
+    S[nb:nb + na, nb:nb + na] = np.tril((H + H.T) / 2 + np.diag(rng.uniform(-3, 3, na)))
+    a0, z0, d0 = nb, nb + na, nb + na + nz
+    S[z0:z0 + nz, a0:a0 + na] = 0.0             # zero block: no pivot among the 60 columns inside the clique
+    S[d0:, :nb] = rng.standard_normal((k, nb)) * 0.05
+    S[d0:, a0:d0] = rng.standard_normal((k, na + nz))
+    S[d0:, d0:] = np.tril(rng.standard_normal((k, k)))
+    S = np.tril(S)
+    # the clique's pattern includes the zero block (explicit zeros): one front of 240 + 150 rows
+    pat = S.copy()
+    pat[z0:z0 + nz, a0:z0 + nz] = np.tril(np.ones((nz, na + nz)), na)
+    r, c = np.nonzero(pat)
+    v = S[r, c]
+    Sf = S + S.T - np.diag(np.diag(S))
+    ev = np.linalg.eigvalsh(Sf)
+    expect = (int((ev > 0).sum()), int((ev < 0).sum()), 0)
+    import uno_amd
+    uno_amd.load_library()
+    o = OracleKKT()
+    o.analyze(n, r, c)
+    o.factorize(v)
+    assert o.inertia() == expect
+    g = uno_amd.HipKKT(0, delay_relaxed=1)
+    g.analyze(n, r, c)
+    g.factorize(v)
+    assert g.inertia() == expect
+    st = g.stats()
+    assert st["fronts_merged"] > 0 and st["max_front"] > 128
+    b = rng.standard_normal(n)
+    x = g.solve(b)
+    assert np.abs(Sf @ x - b).max() < 1e-8 * (np.abs(Sf).sum(1).max() * np.abs(x).max() + np.abs(b).max())

@@ -302,3 +302,40 @@ def test_declined_partition_runs_replicas(ua):
         assert out[q][1]["partitioned"] == 0
         assert out[q][0][0][0] == ine
         np.testing.assert_array_equal(out[q][0][0][1], x)
+
+
+@pytest.mark.gpu
+def test_gate_agrees_across_ranks(ua):
+    """The partition gate is all-reduced: rank 0 would partition (dist_min_efficiency 0), rank 1 declines
+    (dist_min_efficiency 2, unreachable); every rank must take the declined outcome (no rank left waiting in
+    a collective the replicas never join), with the single-GPU inertia and solution on each rank."""
+    n, nv, m, r, c, v, b = ua.arrowband(40000, ua.SEEDS["C2"])
+    single = ua.HipKKT(0)
+    single.analyze(n, r, c)
+    single.factorize(v)
+    ine, x = single.inertia(), single.solve(b)
+    group = ua.LocalGroup(2)
+    out, errs = [None, None], []
+
+    def rank_main(q):
+        try:
+            g = ua.HipKKT(0, dist_min_efficiency=0.0 if q == 0 else 2.0)
+            g.attach_local(group, q)
+            g.analyze(n, r, c)
+            g.factorize(v)
+            out[q] = (g.inertia(), g.solve(b), g.dist_info())
+            g.close()
+        except Exception as e:  # surfaced below
+            errs.append((q, repr(e)))
+
+    th = [threading.Thread(target=rank_main, args=(q,)) for q in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    group.close()
+    assert not errs, errs
+    for q in range(2):
+        assert out[q][2]["partitioned"] == 0
+        assert out[q][0] == ine
+        np.testing.assert_array_equal(out[q][1], x)

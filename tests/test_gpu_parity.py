@@ -178,14 +178,12 @@ def test_random_indefinite(uno_amd, nmax, dens):
     assert done >= 6
 
 
-@pytest.mark.parametrize("mf", [0, 1])
-def test_tile_kernels(uno_amd, mf):
-    """One-wave fronts on either front kernel (option mfma_fronts: the matrix-core tile kernels
-    k_factor_mf / k_factor_df_mf, or the register-grid kernels): inertia equal to the oracle's and the
-    residual bar, on dense indefinite fronts up to 64 rows with zero diagonals (2x2 pivots, interchanges,
-    LDS steps in the middle of a panel) and on the C2 arrowband KKT (level launches + dataflow launch)."""
+def test_small_dense_fronts(uno_amd):
+    """One-wave fronts (register-grid kernels): inertia equal to the oracle's and the residual bar, on
+    dense indefinite fronts up to 64 rows with zero diagonals (2x2 pivots, interchanges, LDS steps in the
+    middle of a panel) and on the C2 arrowband KKT (level launches + dataflow launch)."""
     from uno_amd import arrowband, SEEDS
-    rng = np.random.default_rng(17 + mf)
+    rng = np.random.default_rng(17)
     done = 0
     for trial in range(16):
         n = int(rng.integers(5, 65))
@@ -193,17 +191,42 @@ def test_tile_kernels(uno_amd, mf):
         ev = np.linalg.eigvalsh(S)
         if np.min(abs(ev)) < 1e-8 * max(1.0, abs(ev).max()):
             continue
-        g, o = both(n, rr, cc, vv, mfma_fronts=mf)
+        g, o = both(n, rr, cc, vv)
         assert g.inertia() == o.inertia() == (int((ev > 0).sum()), int((ev < 0).sum()), 0)
         b = rng.standard_normal(n)
         np.testing.assert_allclose(S @ g.solve(b), b, atol=1e-8 * np.linalg.cond(S) * np.abs(b).max())
         done += 1
     assert done >= 8
     n, nv, m, r, c, v, b = arrowband(10000, SEEDS["C2"])
-    g, o = both(n, r, c, v, mfma_fronts=mf)
+    g, o = both(n, r, c, v)
     assert g.inertia() == o.inertia()
     xg = g.solve(b)
     assert rel_residual(n, r, c, v, xg, b) < RES_TOL
+
+
+@pytest.mark.parametrize("rg", [0, 1])
+def test_dataflow_solve_kernels_bit_identical(uno_amd, rg):
+    """C3-shaped arrowband at N = 1e5 (fronts of up to 72 rows, 2x2 pivots): the dataflow solve kernels
+    (rg = 1: register-resident k_solve_{fwd,bwd}_rg, the default; rg = 0: the LDS-panel k_solve_*_df) give
+    solutions bit-identical to the level-scheduled launches, over repeated solves (the arrival counters'
+    epochs) and after a refactorization with new values."""
+    from uno_amd import arrowband, SEEDS, HipKKT
+    n, nv, m, r, c, v, b = arrowband(100000, SEEDS["C3"])
+    gd, gl = HipKKT(0, solve_rg=rg), HipKKT(0, dataflow_solve=0)
+    for g in (gd, gl):
+        g.analyze(n, r, c)
+        g.factorize(v)
+    assert gd.inertia() == gl.inertia()
+    assert gd.stats()["solve_grid"] > 0
+    for rep in range(3):
+        np.testing.assert_array_equal(gd.solve(b * (rep + 1)), gl.solve(b * (rep + 1)))
+    v2 = np.array(v)
+    v2[:n] += 0.5
+    for g in (gd, gl):
+        g.factorize(v2)
+    assert gd.inertia() == gl.inertia()
+    np.testing.assert_array_equal(gd.solve(b), gl.solve(b))
+    assert gd.stats()["solve_aborts"] == 0
 
 
 def test_arrowband_c2(uno_amd):
@@ -354,6 +377,26 @@ def test_threshold_relaxation_with_refinement(uno_amd):
     g.solve_device(bd.data_ptr(), bd.data_ptr())
     torch.cuda.synchronize()
     np.testing.assert_allclose(bd.cpu().numpy(), xg, rtol=1e-12, atol=1e-14 * np.abs(xg).max())
+
+
+def test_refine_tol_non_finite(uno_amd):
+    """Option refine_tol skips the refinement step only when the componentwise backward error of x is
+    finite and below the bound: a NaN in the right-hand side makes omega NaN, which must count as
+    +infinity (the step runs and last_backward_error reports inf), never as a near-perfect solve."""
+    from uno_amd import arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(10000, SEEDS["C2"])
+    g, o = both(n, r, c, v, delay_relaxed=0, refine_tol=1e-6)
+    assert g.stats()["pivots_relaxed"] > 0
+    g.solve(b)
+    st = g.stats()
+    assert 0.0 <= st["last_backward_error"] < np.inf
+    bn = np.array(b)
+    bn[n // 2] = np.nan
+    x = g.solve(bn)
+    st2 = g.stats()
+    assert st2["last_backward_error"] == np.inf
+    assert st2["refinements"] == st["refinements"] + 1 and st2["refinements_skipped"] == st["refinements_skipped"]
+    assert np.isnan(x).any()
 
 
 def test_factorize_update_prefix(uno_amd):

@@ -22,11 +22,11 @@ k = lib.uno_kkt_debug_solve_stamps(g.h, out.ctypes.data_as(ctypes.c_void_p), cty
 assert k == nf, k
 st = out.reshape(nf, 8).astype(np.int64)
 fo = np.zeros(nf, np.int32); fp = np.zeros(nf, np.int32); fl = np.zeros(nf, np.int32)
-lib.uno_kkt_debug_fronts.restype = ctypes.c_int64
-r64 = np.ascontiguousarray(r, np.int64); c64 = np.ascontiguousarray(c, np.int64)
 P = lambda a: a.ctypes.data_as(ctypes.c_void_p)
-nf2 = lib.uno_kkt_debug_fronts(ctypes.c_int64(N), ctypes.c_int64(len(r64)), P(r64), P(c64), P(fo), P(fp), P(fl), ctypes.c_int64(nf))
-levels = fl if nf2 == nf else np.zeros(nf, np.int32)
+lib.uno_kkt_debug_front_info.restype = ctypes.c_int64
+nf2 = lib.uno_kkt_debug_front_info(g.h, P(fo), P(fp), P(fl), ctypes.c_int64(nf))
+assert nf2 == nf, (nf2, nf)
+levels = fl
 for d, name in ((0, "forward"), (4, "backward")):
     s = st[:, d:d + 4]
     t0 = s[:, 0].min()

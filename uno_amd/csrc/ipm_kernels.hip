@@ -274,7 +274,9 @@ __global__ void k_backward_error(const double* __restrict__ r, const double* __r
     double mx = 0.0;
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kT) {
         const double num = fabs(r[i]), den = t[i] + fabs(b[i]);
-        const double w = den > 0.0 ? num / den : (num > 0.0 ? INFINITY : 0.0);
+        double w = den > 0.0 ? num / den : (num > 0.0 ? INFINITY : 0.0);
+        if (!(num <= INFINITY) || !(den <= INFINITY) || !(w <= INFINITY)) w = INFINITY;  // NaN in x, r or b (or
+                                                                                          // inf / inf): forces the refinement step
         mx = fmax(mx, w);
     }
     for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));

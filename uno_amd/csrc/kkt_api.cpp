@@ -188,6 +188,8 @@ struct uno_kkt {
     int32_t n_df_roots = 0, n_df_topf = 0;
     DBuf<unsigned long long> df_abort64;
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
+    int solve_rg = 1;              // option "solve_rg": register-resident dataflow kernels (k_solve_*_rg)
+    int rg_grid_f = 0, rg_grid_b = 0;
     int df_win = 0, df_win_opt = 0; // LDS panel window of the dataflow solve (option solve_window, 0 = auto)
     int df_piv_off = 0;
     uint32_t df_epoch = 0;
@@ -209,11 +211,9 @@ struct uno_kkt {
     hipEvent_t ev_wait = nullptr;      // host_wait_stream
     int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
     bool rmax_clean = false;           // rmax all zero (left so by the front sweeps)
-    int big_app = 1;                   // option "big_app": large fronts by a-posteriori kAppNB-column steps
     int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
                                  // factorization (1), also before every sweep (2)
     int sweep_coalesced = 1;     // option "sweep_coalesced"
-    int wpe2 = 0;                // option "wpe2"
     DBuf<double> fscale;
     DBuf<int8_t> flong;          // per front row: index of its row among the long rows, -1 otherwise
     int dff_enabled = 1;  // 0 off, 1 (default) levels >= L*, 2 also the small fronts below them (measured no faster at C3)
@@ -242,7 +242,6 @@ struct uno_kkt {
     DBuf<double> atmp;                    // |A| |x| of the backward-error check
     DBuf<unsigned long long> omega_d;
     int pin_host = 0;                     // option pin_host_values
-    int mfma_fronts = 0;                  // option mfma_fronts: one-wave fronts on the matrix-core tile kernels
     const double* pinned_ptr = nullptr;   // caller buffer registered with hipHostRegister
     size_t pinned_bytes = 0;
     DBuf<int64_t> edit_pos;               // uno_kkt_set_values staging
@@ -341,7 +340,7 @@ int run_big_fronts(uno_kkt_t h, const FactorArgs& A, const int32_t* fronts, cons
     const int count = L.count, mmax = L.mmax;
     if (count <= 0) return UNO_KKT_OK;
     HIPCHK(h, launch_big_assemble(A, fronts, count, mmax, L.maxch, s));
-    const int nb = big_panel_width(mmax, A.big_app != 0);
+    const int nb = big_panel_width();
     // one panel step per nb pivots of the widest front (+2 for early panel stops before the first check)
     int batch = (L.pmax + nb - 1) / nb + 2;
     int64_t steps = 0;
@@ -451,18 +450,7 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
         // front).  Finer LDS classes ({16, 24, .., 128}) were measured slower on C3 (2.36 vs 1.99 ms):
         // the one-wave kernel is VALU-issue bound at levels 0-1 and more co-resident fronts per CU
         // only lengthen every front; a class smaller than kMinClass absorbs the next smaller one.
-        static const std::vector<int> caps = [] {  // UNO_KKT_CAPS="32,48,64,72,128" (experiments)
-            std::vector<int> c{32, 64, kMaxWaveFront, 128};
-            if (const char* e = getenv("UNO_KKT_CAPS")) {
-                c.clear();
-                for (const char* p = e; *p;) {
-                    c.push_back(atoi(p));
-                    while (*p && *p != ',') ++p;
-                    if (*p) ++p;
-                }
-            }
-            return c;
-        }();
+        static const std::vector<int> caps{32, 64, kMaxWaveFront, 128};  // LDS size classes
         constexpr int kMinClass = 2048;
         auto prev_cap = [](int c) {
             int pc = 0;
@@ -1002,6 +990,8 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     h->df_lds = lds;
     h->df_nwalk = (int32_t)walk.size();
     h->df_grid = solve_df_grid(lds, h->df_nwalk);
+    h->rg_grid_f = solve_rg_grid(true, h->df_nwalk);
+    h->rg_grid_b = solve_rg_grid(false, h->df_nwalk);
     if (h->verbose)
         fprintf(stderr, "[uno_kkt] dataflow solve: %d of %lld fronts, panel window %d of %d doubles, lds %d doubles, grid %d\n",
                 h->df_nwalk, (long long)S.nf, win, max_sz, lds, h->df_grid);
@@ -1311,12 +1301,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
-    A.mf = h->mfma_fronts;
-    A.wpe2 = h->wpe2;
-    static const int diag_nopiv = getenv("UNO_KKT_DIAG_NOPIV") ? atoi(getenv("UNO_KKT_DIAG_NOPIV")) : 0;
-    A.diag_nopiv = diag_nopiv;
     A.big = h->big.p;
-    A.big_app = h->big_app;
     if (h->last_optimistic) A.anorm_bits = nullptr;
     A.fparent = h->fparent.p; A.delayed = h->delayed.p; A.record_delays = h->delay_relaxed;
     A.stamps = nullptr;
@@ -1500,7 +1485,6 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "refine_tol") h->refine_tol = std::max(0.0, value);
     else if (n == "pin_host_values") h->pin_host = value != 0.0;
-    else if (n == "mfma_fronts") h->mfma_fronts = value != 0.0;
     else if (n == "front_sweeps") h->front_sweeps = value != 0.0;
     else if (n == "stamps") h->want_stamps = (int)value;
     else if (n == "max_merge_rounds") h->max_merge_rounds = std::max(0, (int)value);
@@ -1511,10 +1495,8 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
     else if (n == "early_xpos") h->early_xpos = value != 0.0;
     else if (n == "spin_wait") h->spin_wait = value != 0.0;
-    else if (n == "big_app") h->big_app = value != 0.0;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
     else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
-    else if (n == "wpe2") h->wpe2 = value != 0.0;
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;
     else if (n == "dist_force") h->dist_force = value != 0.0;
@@ -1539,6 +1521,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }
+    else if (n == "solve_rg") h->solve_rg = value != 0.0;
     else if (n == "dataflow_solve") {
         h->df_enabled = value != 0.0;
         if (h->analyzed) {
@@ -1566,7 +1549,8 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
     // parallelism"): the subtree partition is used only if it has at least `world` subtrees and its estimated
     // parallel efficiency total / (world * (max rank work + top work)) reaches dist_min_efficiency; otherwise
     // every rank factors and solves the whole matrix on its own GPU (replicas, no collective).  The decision
-    // is a pure function of the pattern, so every rank takes the same one; delayed-pivot rebuilds keep it.
+    // is a pure function of the pattern and the options, all-reduced so every rank takes the same one;
+    // delayed-pivot rebuilds keep it.
     h->world = h->comm_world;
     h->rank = h->comm_rank;
     h->dist_declined = false;
@@ -1576,7 +1560,19 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
         partition_tree(h->S, h->world, Pt);
         const double denom = (double)h->world * (Pt.max_rank_work + Pt.top_work);
         h->dist_efficiency = denom > 0.0 ? Pt.total_work / denom : 0.0;
-        if (!h->dist_force && (Pt.n_subtrees < h->world || h->dist_efficiency < h->dist_min_eff)) {
+        bool decline = !h->dist_force && (Pt.n_subtrees < h->world || h->dist_efficiency < h->dist_min_eff);
+        {
+            // the ranks agree on the gate even if their options differ: any rank declining makes all decline
+            // (otherwise a partitioned rank would wait in collectives a replica never joins)
+            if (!h->df_abort64.p) HIPCHK(h, h->df_abort64.alloc(1));
+            unsigned long long flag = decline ? 1ull : 0ull;
+            HIPCHK(h, hipMemcpyAsync(h->df_abort64.p, &flag, sizeof(flag), hipMemcpyHostToDevice, h->stream));
+            HIPCHK(h, h->comm->allreduce(h->df_abort64.p, 1, RedOp::MaxU64, h->stream));
+            HIPCHK(h, hipMemcpyAsync(&flag, h->df_abort64.p, sizeof(flag), hipMemcpyDeviceToHost, h->stream));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+            decline = flag != 0;
+        }
+        if (decline) {
             h->dist_declined = true;
             h->world = 1;
             h->rank = 0;
@@ -1756,6 +1752,11 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
         HIPCHK(h, launch_rhs_scale(b, h->scale.p, h->w.p, S.n, s));
     }
     DfArgs Df;
+    auto walk = [&](bool forward) -> hipError_t {
+        const int g = forward ? h->rg_grid_f : h->rg_grid_b;
+        if (h->solve_rg && forward && g > 0) return launch_solve_rg(A, Df, g, forward, s);
+        return launch_solve_df(A, Df, h->df_grid, h->df_lds, forward, s);
+    };
     if (df) {
         Df = dataflow_args(h);
         if (!h->df_rx_valid) {
@@ -1779,11 +1780,11 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
         }
         {
             TimerScope t(h, KC_SOLVE_FWD);
-            HIPCHK(h, launch_solve_df(A, Df, h->df_grid, h->df_lds, true, s));
+            HIPCHK(h, walk(true));
         }
         if (!dist) {
             TimerScope t(h, KC_SOLVE_BWD);
-            HIPCHK(h, launch_solve_df(A, Df, h->df_grid, h->df_lds, false, s));
+            HIPCHK(h, walk(false));
         }
     }
     for (size_t q = 0; q < P0.sol.size() && !df; ++q) {
@@ -1819,7 +1820,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
         if (df) {  // the subtree roots' parents (top fronts) have published
             HIPCHK(h, launch_set_done(h->df_done.p, h->df_topf.p, h->n_df_topf, Df.epoch, s));
             TimerScope t(h, KC_SOLVE_BWD);
-            HIPCHK(h, launch_solve_df(A, Df, h->df_grid, h->df_lds, false, s));
+            HIPCHK(h, walk(false));
         }
     }
     for (size_t q = P0.sol.size(); q-- > 0 && !df;) {
@@ -2052,6 +2053,14 @@ int64_t uno_kkt_debug_solve_stamps(uno_kkt_t h, uint64_t* out, int64_t cap) {
     if (cap < 8 * nf) return -(8 * nf);
     HIPCHK(h, hipStreamSynchronize(h->stream));
     HIPCHK(h, hipMemcpy(out, h->df_stamps.p, sizeof(uint64_t) * 8 * nf, hipMemcpyDeviceToHost));
+    return nf;
+}
+
+int64_t uno_kkt_debug_front_info(uno_kkt_t h, int32_t* fm, int32_t* fp, int32_t* flevel, int64_t cap) {
+    if (!h) return -1;
+    const int64_t nf = h->S.nf;
+    if (cap < nf) return -nf;
+    for (int64_t f = 0; f < nf; ++f) { fm[f] = h->S.f_m[f]; fp[f] = h->S.f_p[f]; flevel[f] = h->S.f_level[f]; }
     return nf;
 }
 

@@ -574,7 +574,6 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
             if (q >= m) continue;
             const unsigned long long bw = rm[q];
             if (lk[u] >= 0) A.part_long[(int64_t)f * A.n_long + lk[u]] = as_double(bw);  // every front writes its slot
-            else if (A.diag_noatomic) A.part_long[rr[u] & 1023] = as_double(bw);  // diagnostics: timing without atomics
             else if (bw != 0ull) atomicMax(A.rmax + rr[u], bw);
         }
         return;
@@ -1080,13 +1079,6 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         if (W > 1 && tid == 0) sh->failk = -1;
         reg_load<G, RM>(st, m, R);
     }
-    if (A.diag_nopiv) {  // timing diagnostics only: no pivot steps (every column written as a 1x1 pivot)
-        for (int i = tid; i < p; i += NT) piv[i] = PIV_1X1;
-        __syncthreads();
-        k = p;
-        npos = p;
-        spilled = true;
-    }
     while (k < p) {
         if constexpr (REG && W == 1) {
             // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of
@@ -1292,7 +1284,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         // L of the columns pivoted by the register path: column j (< p) still holds A(i, j) as it
         // was at step j, so L(i, j) = A(i, j) / d_j and L(j, j) = d_j, stored straight from the
         // registers (for a fixed register, the 8 lanes of a column group write 8 consecutive rows)
-        if (fastmask && !(A.diag_nopiv & 2)) {
+        if (fastmask) {
             const int ty = tid / G, tx = tid % G;
 #pragma unroll
             for (int b = 0; b < RM; ++b) {
@@ -1311,7 +1303,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         }
     }
     // columns still to be written from the LDS front (all when no register path ran)
-    const bool lds_L = !(A.diag_nopiv & 2) && (!(REG && W == 1) || fastmask != (p >= 64 ? ~0ull : ((1ull << p) - 1)));
+    const bool lds_L = !(REG && W == 1) || fastmask != (p >= 64 ? ~0ull : ((1ull << p) - 1));
     const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
@@ -1411,7 +1403,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     if (sub) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
     // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
-    const int cm = (A.diag_nopiv & 4) ? 0 : m - p;
+    const int cm = m - p;
     if constexpr (REG && W == 1) {
         // contribution block straight from the registers: element (i, j), p <= j <= i < m
         if (cm > 0) {
@@ -1561,7 +1553,7 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
     const bool asm_st = A.stamps && A.stamp_mode == 4 && tid == 0;  // diagnostics: assembly sub-phases
     if (asm_st) A.stamps[8 * f + 4] = __builtin_amdgcn_s_memrealtime();
     // original entries (distinct positions, summed duplicates already packed by k_pack)
-    for (int64_t eb = e0 + tid; !(A.diag_nopiv & 8); eb += (int64_t)EB * NT) {
+    for (int64_t eb = e0 + tid;; eb += (int64_t)EB * NT) {
 #pragma unroll
         for (int q = 0; q < EB; ++q) {
             const int64_t e = eb + (int64_t)q * NT;
@@ -1614,7 +1606,7 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
 #pragma unroll
         for (int u = 0; u < CB; ++u) st.F[b.pos[u]] = old[u] + b.v[u];
     };
-    for (int cb0 = c0; cb0 < c1 && !(A.diag_nopiv & 8); cb0 += 64) {
+    for (int cb0 = c0; cb0 < c1; cb0 += 64) {
         if (cb0 != c0 && lane < c1 - cb0) {
             my_cm = A.ch_cm[cb0 + lane];
             my_rmo = (unsigned long long)A.ch_relmap_off[cb0 + lane];
@@ -1706,442 +1698,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     assemble_front<64, true>(st, fsize, m, p, lrow, sloc, rstage, A, f);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
     factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
-    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
-    const int par = A.fparent[f];
-    drain_stores();
-    if (par >= 0 && threadIdx.x == 0) __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// ------------------------------------------------------------------------------------------------
-// One-wave front factorization on matrix-core tiles (fronts of m <= 16 * TR rows)
-// ------------------------------------------------------------------------------------------------
-// The front lives in registers as the lower triangle of TR x TR tiles of 16 x 16 in the
-// v_mfma_f64_16x16x4f64 C layout (lane l: column l & 15, rows (l >> 4) + 4 r; MI355X_MICROARCH.md,
-// f64 MFMA).  Fully-summed columns are eliminated in panels of at most one tile column: the panel is
-// transposed through an LDS stage into a row-per-lane copy P (lane i = row i), where a pivot step is
-// one per-lane threshold compare + one ballot (the Duff-Reid 1x1 rule of factor_front's fast path),
-// one division and the update of the panel's later pivot columns with readlane operands -- no LDS
-// round trip per pivot.  L of each pivot goes to HBM at once.  At the end of the panel the eliminated
-// columns W (staged in LDS) update every trailing tile on the matrix cores, C -= W (W D^-1)^T: the
-// same products A(i,k) * (A(j,k) / d_k) as the one-pivot updates.  A pivot that fails the quick test
-// flushes the pending update, spills the live tiles to the packed LDS front and takes one LDS step of
-// the full search (interchanges, 2x2, null pivots, relaxation, delays) before the tiles are reloaded.
-constexpr int kStageLd = 17;  // row stride (doubles) of the LDS panel stage
-
-// doubles of the front region of the tile kernels: the packed triangle or the panel stage (rows of
-// whole tiles), whichever is larger; monotone in m, so factor_lds_bytes(mmax) covers every m <= mmax
-__host__ __device__ __forceinline__ int64_t mf_front_doubles(int m) {
-    const int64_t pk = (((int64_t)m * (m + 1) / 2) + 1) & ~1ll;
-    const int64_t sg = (((int64_t)16 * ((m + 15) >> 4) * kStageLd) + 1) & ~1ll;
-    return pk > sg ? pk : sg;
-}
-
-template <int TR>
-__device__ __forceinline__ void mf_load(const PackedStore& st, int m, dbl4 (&acc)[TR * (TR + 1) / 2]) {
-    int lane = threadIdx.x & 63;
-    asm volatile("" : "+v"(lane));
-    const int g = lane >> 4, c = lane & 15;
-    const int ntr = (m + 15) >> 4;
-#pragma unroll
-    for (int tr = 0; tr < TR; ++tr) {
-        if (tr >= ntr) break;  // uniform
-#pragma unroll
-        for (int tc = 0; tc < TR; ++tc) {
-            if (tc > tr) break;
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * tr + g + 4 * r, j = 16 * tc + c;
-                const bool ok = i < m && j <= i;
-                const double v = st.F[ok ? st.idx(i, j) : -1];
-                acc[tr * (tr + 1) / 2 + tc][r] = ok ? v : 0.0;
-            }
-        }
-    }
-}
-
-// live part (columns >= k) of the tiles -> packed LDS front
-template <int TR>
-__device__ __forceinline__ void mf_spill(const PackedStore& st, int m, int k, const dbl4 (&acc)[TR * (TR + 1) / 2]) {
-    int lane = threadIdx.x & 63;
-    asm volatile("" : "+v"(lane));
-    const int g = lane >> 4, c = lane & 15;
-    const int ntr = (m + 15) >> 4;
-#pragma unroll
-    for (int tr = 0; tr < TR; ++tr) {
-        if (tr >= ntr) break;
-#pragma unroll
-        for (int tc = 0; tc < TR; ++tc) {
-            if (tc > tr) break;
-            if (16 * tc + 15 < k) continue;  // uniform: tile column entirely eliminated
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int i = 16 * tr + g + 4 * r, j = 16 * tc + c;
-                st.F[(i < m && j >= k && j <= i) ? st.idx(i, j) : -1] = acc[tr * (tr + 1) / 2 + tc][r];
-            }
-        }
-    }
-}
-
-// A later LDS step interchanged rows a < b: the L columns [0, ncols) already in HBM trade those rows.
-// This wave's stores are drained first and the rows are read back through L2 (sc1).
-__device__ __forceinline__ void mf_swap_L(double* Lf, int m, int ncols, int a, int b) {
-    drain_stores();
-    for (int j = threadIdx.x & 63; j < ncols; j += 64) {
-        double* Lj = Lf + (int64_t)j * m - (int64_t)j * (j - 1) / 2 - j;
-        const double x = ld_sc1(Lj + a), y = ld_sc1(Lj + b);
-        Lj[a] = y;
-        Lj[b] = x;
-    }
-    drain_stores();
-}
-
-// L of the column(s) [k, k + nk) eliminated by an LDS step, from the packed front (factor_front's
-// write-out formulas: D on the diagonal / 2x2 block, L(i, j) = cA A(i, base) + cB A(i, base + 1))
-__device__ __forceinline__ void mf_write_L_lds(const PackedStore& st, double* Lf, int m, int k, int nk, const int8_t* piv) {
-    const int lane = threadIdx.x & 63;
-    for (int j = k; j < k + nk; ++j) {
-        const int8_t kind = piv[j];
-        double ca = 0.0, cbv = 0.0;
-        int base = j;
-        if (kind == PIV_1X1) {
-            ca = 1.0 / st.at(j, j);
-        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
-            const int k0 = kind == PIV_2X2_A ? j : j - 1;
-            const double a = st.at(k0, k0), b = st.at(k0 + 1, k0), e = st.at(k0 + 1, k0 + 1);
-            const double idet = 1.0 / (a * e - b * b);
-            if (kind == PIV_2X2_A) { ca = e * idet; cbv = -b * idet; }
-            else { ca = -b * idet; cbv = a * idet; base = j - 1; }
-        }
-        double* Lj = Lf + (int64_t)j * m - (int64_t)j * (j - 1) / 2 - j;
-        for (int i = j + lane; i < m; i += 64) {
-            double v;
-            if (i == j) v = kind == PIV_NULL ? 0.0 : st.at(j, j);
-            else if (kind == PIV_2X2_A && i == j + 1) v = st.at(j + 1, j);
-            else {
-                v = ca * st.at(i, base);
-                if (kind >= PIV_2X2_A) v += cbv * st.at(i, base + 1);
-            }
-            Lj[i] = v;
-        }
-    }
-}
-
-template <int TR, bool DF>
-__device__ void factor_front_mf(const PackedStore& st, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
-                                double* dinvs, const FactorArgs& A, int f, FrontShared* sh) {
-    constexpr int NTL = TR * (TR + 1) / 2;
-    constexpr int RPL = (16 * TR + 63) / 64;  // panel rows per lane
-    const int tid = threadIdx.x;
-    const int lane = tid & 63, g = lane >> 4, cl = lane & 15;
-    const int ntr = (m + 15) >> 4;
-    for (int i = tid; i < m; i += 64) lorig[i] = i;
-    __syncthreads();
-    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
-    double minpiv = INFINITY;
-    long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
-    bool delays_recorded = false;
-    double* Lf = A.L + A.L_off[f];
-    double* S = st.F;  // panel stage: aliases the packed front, dead while the tiles hold the front
-    dbl4 acc[NTL];
-    mf_load<TR>(st, m, acc);
-    // diagnostics (stamp_mode 5): shader cycles of extraction / pivots / stage + MFMA / LDS steps
-    const bool stamping = A.stamps != nullptr && A.stamp_mode == 5;
-    unsigned long long cyc[4] = {0, 0, 0, 0}, t_mark = 0;
-    int k = 0;
-    while (k < p) {
-        if (stamping) t_mark = __builtin_amdgcn_s_memtime();
-        const int tc = k >> 4, j0 = k & 15;
-        const int jlim = min(16, p - 16 * tc);  // panel: pivot columns [16 tc + j0, 16 tc + jlim)
-        // ---- tile column tc -> LDS stage -> row-per-lane panel P (upper part and rows >= m zero) ----
-#pragma unroll
-        for (int TC = 0; TC < TR; ++TC) {
-            if (TC != tc) continue;  // uniform: static tile indices
-            int gg = g, cc = cl;
-            asm volatile("" : "+v"(gg), "+v"(cc));
-            double* dst = S + gg * kStageLd + cc;
-#pragma unroll
-            for (int tr = 0; tr < TR; ++tr) {
-                if (tr < TC) continue;
-                if (tr >= ntr) break;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) dst[(16 * tr + 4 * r) * kStageLd] = acc[tr * (tr + 1) / 2 + TC][r];
-            }
-        }
-        double P[RPL][16];
-#pragma unroll
-        for (int rr = 0; rr < RPL; ++rr) {
-            int i = lane + 64 * rr;
-            asm volatile("" : "+v"(i));  // per-section addresses (not hoisted into live registers)
-            const bool rowok = i < m && i >= 16 * tc;
-            const double* src = S + (rowok ? i : 16 * tc) * kStageLd;  // one base, immediate offsets
-            double v[16];
-#pragma unroll
-            for (int c = 0; c < 16; ++c) v[c] = src[c];
-            // keep the reads unconditional (all issued before the first wait): sunk under the masks below
-            // they become one divergent branch + LDS wait per element
-#pragma unroll
-            for (int c = 0; c < 16; ++c) asm volatile("" : "+v"(v[c]));
-            // lower part of the live columns only: upper entries, rows >= m and columns eliminated before
-            // this panel read as 0 (the update below keeps them 0: its row factor is 0 there)
-#pragma unroll
-            for (int c = 0; c < 16; ++c) P[rr][c] = (rowok && i >= 16 * tc + c && c >= j0) ? v[c] : 0.0;
-        }
-        if (stamping) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cyc[0] += t - t_mark; t_mark = t; }
-        // ---- pivots of the panel: quick 1x1 test, L to HBM, update of the later panel columns ----
-        // Column jj is broadcast through an LDS vector (the stage is free between the extraction and the
-        // W stage): the pivot and the panel's row kk come back as uniform broadcast reads, so a step costs
-        // the test, one division, the L store and one FMA per later panel column on the vector ALU.
-        double* vec = S;
-        bool need = false;
-        int jend = j0;
-#pragma unroll
-        for (int jj = 0; jj < 16; ++jj) {
-            if (jj < j0 || jj >= jlim || need) continue;  // uniform
-            const int kk = 16 * tc + jj;
-#pragma unroll
-            for (int rr = 0; rr < RPL; ++rr) vec[lane + 64 * rr] = P[rr][jj];
-            const double akk = vec[kk];
-            double sv[16];
-#pragma unroll
-            for (int c = 0; c < 16; c += 2) {  // 16-byte broadcast reads of the panel rows 16 tc .. 16 tc + 15
-                sv[c] = vec[16 * tc + c];
-                sv[c + 1] = vec[16 * tc + c + 1];
-            }
-            const double aak = fabs(akk);
-            bool bad = false;
-#pragma unroll
-            for (int rr = 0; rr < RPL; ++rr) {
-                const int i = lane + 64 * rr;
-                bad |= i > kk && i < m && A.u * fabs(P[rr][jj]) > aak;
-            }
-            need = (__ballot(bad) != 0) || !(aak > thres);
-            if (need) continue;
-            minpiv = fmin(minpiv, aak);
-            const double dinv = 1.0 / akk;
-            double* Lj = Lf + (int64_t)kk * m - (int64_t)kk * (kk - 1) / 2 - kk;  // L(i, kk) = Lj[i]
-            double li[RPL];
-#pragma unroll
-            for (int rr = 0; rr < RPL; ++rr) {
-                const int i = lane + 64 * rr;
-                const double l = P[rr][jj] * dinv;
-                li[rr] = i > kk ? l : 0.0;
-                if (i >= kk && i < m) Lj[i] = i == kk ? akk : l;
-            }
-            dinvs[kk] = dinv;  // every lane stores the same value (no divergent branch)
-            piv[kk] = PIV_1X1;
-            if (akk > 0.0) npos++; else nneg++;
-#pragma unroll
-            for (int c = 1; c < 16; ++c) {
-                if (c <= jj) continue;
-                if (c >= jlim) break;  // uniform
-#pragma unroll
-                for (int rr = 0; rr < RPL; ++rr) P[rr][c] -= li[rr] * sv[c];  // A(i,c) -= L(i,kk) A(c,kk)
-            }
-            jend = jj + 1;
-        }
-        if (stamping) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cyc[1] += t - t_mark; t_mark = t; }
-        if (jend > j0) {
-            // ---- panel columns W -> stage; trailing tiles on MFMA: C -= (W D^-1) W^T over the eliminated
-            // columns (the L side is zero for the panel columns not eliminated here) ----
-#pragma unroll
-            for (int rr = 0; rr < RPL; ++rr) {
-                int i = lane + 64 * rr;
-                asm volatile("" : "+v"(i));
-                if (i < 16 * ntr) {
-                    double* dst = S + i * kStageLd;
-#pragma unroll
-                    for (int c = 0; c < 16; ++c) dst[c] = P[rr][c];
-                }
-            }
-#pragma unroll
-            for (int TC = 0; TC < TR; ++TC) {
-                if (TC != tc) continue;
-#pragma unroll
-                for (int kc = 0; kc < 4; ++kc) {
-                    if (4 * kc + 4 <= j0 || 4 * kc >= jend) continue;  // uniform: no pivot of this k-chunk
-                    double w[TR];
-                    int gg = g, cc = cl;
-                    asm volatile("" : "+v"(gg), "+v"(cc));
-                    const double* src = S + cc * kStageLd + gg;
-#pragma unroll
-                    for (int tr = 0; tr < TR; ++tr) {
-                        if (tr < TC) continue;
-                        w[tr] = tr < ntr ? src[16 * tr * kStageLd + 4 * kc] : 0.0;  // uniform condition
-                    }
-                    const int col = 4 * kc + gg;
-                    const bool cok = col >= j0 && col < jend;
-                    const double dv = dinvs[cok ? 16 * tc + col : 0];
-                    const double dsel = cok ? -dv : 0.0;
-#pragma unroll
-                    for (int tr = 0; tr < TR; ++tr) {
-                        if (tr < TC) continue;
-                        if (tr >= ntr) break;
-                        const double lop = w[tr] * dsel;  // -L(16 tr + (l & 15), column) on the A side
-#pragma unroll
-                        for (int tcp = 0; tcp < TR; ++tcp) {
-                            if (tcp < TC) continue;
-                            if (tcp > tr) break;
-                            acc[tr * (tr + 1) / 2 + tcp] =
-                                __builtin_amdgcn_mfma_f64_16x16x4f64(lop, w[tcp], acc[tr * (tr + 1) / 2 + tcp], 0, 0, 0);
-                        }
-                    }
-                }
-            }
-        }
-        k = 16 * tc + jend;
-        if (stamping) {
-            __builtin_amdgcn_s_waitcnt(0);
-            const unsigned long long t = __builtin_amdgcn_s_memtime();
-            cyc[2] += t - t_mark;
-            t_mark = t;
-        }
-        if (!need) continue;
-        // ---- pivot k failed the quick test: one LDS step of the full search (factor_front's LDS path) ----
-        mf_spill<TR>(st, m, k, acc);
-        __syncthreads();
-        PivotDecision d = search_pivot(st, m, k, p, A.u, thres, minpiv);  // wave-uniform
-        const bool stuck = d.kind == PIV_STUCK;
-        if (stuck) { d.kind = PIV_NULL; d.c = k; }
-        if (d.c != k) {
-            sym_swap<64>(st, m, k, d.c, lrow, lorig);
-            __syncthreads();
-            mf_swap_L(Lf, m, k, k, d.c);
-        }
-        if (d.kind == PIV_2X2_A) {
-            const int r = d.r == k ? d.c : d.r;
-            if (r != k + 1) {
-                sym_swap<64>(st, m, k + 1, r, lrow, lorig);
-                __syncthreads();
-                mf_swap_L(Lf, m, k, k + 1, r);
-            }
-        }
-        if (tid == 0) {
-            if (stuck) nstuck++;
-            nrel += d.relaxed;
-            // first pivot that needed a relaxed threshold: the columns still fully summed would be delayed
-            // by MUMPS; report them (except at roots) so the host moves them to the parent
-            if (d.relaxed && !delays_recorded && A.record_delays && A.fparent[f] >= 0) {
-                delays_recorded = true;
-                unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
-                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
-            }
-        }
-        int nk;
-        if (d.kind == PIV_NULL) {
-            for (int i = k + 1 + tid; i < m; i += 64) st.at(i, k) = 0.0;
-            piv[k] = PIV_NULL;
-            nzero++;
-            nk = 1;
-        } else if (d.kind == PIV_1X1) {
-            const double dk = st.at(k, k);
-            schur_update_generic<8, false>(st, m, k, 1.0 / dk, 0.0, 0.0);
-            piv[k] = PIV_1X1;
-            if (dk > 0.0) npos++; else nneg++;
-            nk = 1;
-        } else {  // 2x2
-            const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
-            const double det = a * e - b * b;
-            const double idet = 1.0 / det;
-            schur_update_generic<8, true>(st, m, k, a * idet, b * idet, e * idet);
-            piv[k] = PIV_2X2_A;
-            piv[k + 1] = PIV_2X2_B;
-            n2++;
-            if (det < 0.0) { npos++; nneg++; }
-            else if (a + e > 0.0) npos += 2;
-            else nneg += 2;
-            nk = 2;
-        }
-        __syncthreads();
-        mf_write_L_lds(st, Lf, m, k, nk, piv);
-        k += nk;
-        mf_load<TR>(st, m, acc);
-        if (stamping) { const unsigned long long t = __builtin_amdgcn_s_memtime(); cyc[3] += t - t_mark; }
-    }
-    if (stamping && tid == 0)
-        for (int q = 0; q < 4; ++q) A.stamps[8 * f + 4 + q] = cyc[q];
-    if (A.stamps && tid == 0) A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
-    // ---- permuted row ids and pivot kinds ----
-    for (int i = tid; i < m; i += 64) {
-        A.frow[A.rows_off[f] + i] = lrow[i];
-        A.fpos[A.rows_off[f] + lorig[i]] = i;
-        if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
-    }
-    // ---- contribution block (row-major packed lower triangle of order m - p) from the tiles ----
-    if (m > p) {
-        double* cb = A.cb + A.cb_off[f];
-#pragma unroll
-        for (int tr = 0; tr < TR; ++tr) {
-            if (tr >= ntr) break;
-            if (16 * tr + 15 < p) continue;  // uniform: tile rows entirely pivot rows
-#pragma unroll
-            for (int tc = 0; tc < TR; ++tc) {
-                if (tc > tr) break;
-                if (16 * tc + 15 < p) continue;
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int i = 16 * tr + g + 4 * r, j = 16 * tc + cl;
-                    if (i < m && j >= p && j <= i) {
-                        double* dst = cb + ((i - p) * (i - p + 1)) / 2 + (j - p);
-                        if (DF) st_sc1(dst, acc[tr * (tr + 1) / 2 + tc][r]);
-                        else *dst = acc[tr * (tr + 1) / 2 + tc][r];
-                    }
-                }
-            }
-        }
-    }
-    if (tid == 0) {
-        A.fstat[f] = (int32_t)((nstuck > 0xffff ? 0xffff : nstuck) | ((nrel > 0x7fff ? 0x7fff : nrel) << 16));
-        A.fcnt[f] = (unsigned long long)npos | (unsigned long long)nneg << 16 | (unsigned long long)nzero << 32 |
-                    (unsigned long long)n2 << 48;
-        A.fmin[f] = minpiv;
-    }
-}
-
-// LDS layout of the tile kernels: [FrontShared 32 B][front region mf_front_doubles(m)][sloc m][dinvs m]
-// [lrow m][lorig m][piv m]
-template <int TR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(TR > 2 ? 2 : 3))) void k_factor_mf(FactorArgs A, const int32_t* __restrict__ fronts) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
-    const int f = fronts[blockIdx.x];
-    const int m = A.fm[f], p = A.fp[f];
-    const PackedStore st{smem + 4};
-    const int64_t fsize = mf_front_doubles(m);
-    double* sloc = smem + 4 + fsize;
-    double* dinvs = sloc + m;
-    int32_t* lrow = (int32_t*)(dinvs + m);
-    int32_t* lorig = lrow + m;
-    int8_t* pk = (int8_t*)(lorig + m);
-    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
-    assemble_front<64, false>(st, packed_even(m), m, p, lrow, sloc, lorig, A, f);
-    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front_mf<TR, false>(st, m, p, lrow, lorig, pk, dinvs, A, f, sh);
-    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
-}
-
-// k_factor_df on the tile factorization (same ticket / arrival-counter protocol)
-template <int TR>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_factor_df_mf(FactorArgs A) {
-    extern __shared__ __attribute__((aligned(16))) double smem[];
-    FrontShared* sh = reinterpret_cast<FrontShared*>(smem);
-    uint32_t tk = 0;
-    if (threadIdx.x == 0) tk = __hip_atomic_fetch_add(A.df_ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    tk = (uint32_t)__builtin_amdgcn_readfirstlane((int)tk);
-    const int t = (int)(tk - (A.df_epoch - 1u) * (uint32_t)A.df_nf);
-    if (t < 0 || t >= A.df_nf) return;
-    const int f = A.df_order[t];
-    const int m = A.fm[f], p = A.fp[f];
-    const PackedStore st{smem + 4};
-    const int64_t fsize = mf_front_doubles(m);
-    double* sloc = smem + 4 + fsize;
-    double* dinvs = sloc + m;
-    int32_t* lrow = (int32_t*)(dinvs + m);
-    int32_t* lorig = lrow + m;
-    int8_t* pk = (int8_t*)(lorig + m);
-    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
-    assemble_front<64, true>(st, packed_even(m), m, p, lrow, sloc, lorig, A, f);
-    if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front_mf<TR, true>(st, m, p, lrow, lorig, pk, dinvs, A, f, sh);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
     const int par = A.fparent[f];
     drain_stores();
@@ -2566,6 +2122,7 @@ __global__ __launch_bounds__(64) void k_solve_bwd_w(SolveArgs A, const int32_t* 
 // solution gathered out by k_xs_in / k_xs_out), so a front's own values need no row-id round trip.
 // A front then costs one dependent round trip (its children's / ancestors' values), its arithmetic
 // and the store drain before its signal.
+__device__ __forceinline__ int cstart(int m, int k) { return k * m - ((k * (k - 1)) >> 1); }  // flat index of L(k, k)
 __device__ __forceinline__ int col_start(int m, int k) { return k * m - k * (k - 1) / 2; }  // flat index of L(k, k)
 __device__ __forceinline__ int fwd_chunk_end(int m, int p, int k0, int win) {
     int k1 = k0, used = 0;
@@ -2807,6 +2364,138 @@ __device__ __forceinline__ double bwd_compute_win(const double* __restrict__ L, 
     return xj;
 }
 
+// Round 4: the pivot-step loops of fwd_compute_win / bwd_compute_win, unrolled by 8 with the 8 steps' LDS
+// operands read before the first step (no LDS latency on the dependency chain), pivot kinds as wave-uniform
+// ballot masks (scalar bit tests, no branch per step), and lane = row in the forward (rows < 64 in y0,
+// rows >= 64 in a1).  The per-row / per-column sequence of operations is unchanged: bit-identical results.
+__device__ __forceinline__ void fwd_compute_win2(const double* __restrict__ L, int64_t Lo, int m, int p, double* P, int win,
+                                                 int k1, double* y, int mypiv, double* zdst, double* cvo) {
+    const int lane = threadIdx.x;
+    const bool two = m > 64;  // uniform
+    const unsigned long long liveM = __ballot(lane < p && mypiv != PIV_NULL);
+    const unsigned long long twoAM = __ballot(lane < p && mypiv == PIV_2X2_A);
+    double y0 = y[lane];
+    double a1 = two && lane + 64 < m ? y[lane + 64] : 0.0;
+    double dg = 0.0, sb = 0.0;
+    const int csl = cstart(m, lane);                      // lane's own column start (pivot lanes)
+    const int csp = lane > 0 ? cstart(m, lane - 1) : 0;   // and its predecessor's
+    int base = 0, k = 0, cs = 0;                          // cs = cstart(m, k)
+    for (;;) {
+        while (k < k1) {
+            const int kend = min(k + 8, k1);
+            double l0[8], l1[8];
+            int c = cs;
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int kk = k + u;
+                if (kk < kend) {  // uniform
+                    const int o = c - base - kk;  // P[o + i] = L(i, kk)
+                    l0[u] = P[max(o + lane, 0)];
+                    l1[u] = two ? P[o + 64 + lane] : 0.0;
+                    c += m - kk;
+                }
+            }
+            if (lane >= k && lane < kend) dg = P[csl - base];           // D(k, k) of the chunk's pivots
+            if (lane > k && lane <= kend && lane - 1 < p) sb = P[csp - base + 1];  // L(k + 1, k)
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int kk = k + u;
+                if (kk < kend) {  // uniform
+                    const double yb = readlane_d(y0, kk);
+                    const double yk = (liveM >> kk) & 1 ? yb : 0.0;
+                    const int lim = (twoAM >> kk) & 1 ? kk + 1 : kk;
+                    const double t = y0 - l0[u] * yk;
+                    y0 = lane > lim ? t : y0;
+                    a1 -= l1[u] * yk;
+                }
+            }
+            k = kend;
+            cs = c;
+        }
+        if (k >= p) break;
+        base = cs;
+        k1 = fwd_chunk_end(m, p, k, win);
+        __syncthreads();
+        stage_panel<4>(L, Lo + base, cstart(m, k1) - base, P);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window's loads are all consumed here
+        __syncthreads();
+    }
+    if (lane >= p && lane < m) st_sc1(cvo + (lane - p), y0);
+    if (two && lane + 64 < m) st_sc1(cvo + (lane + 64 - p), a1);
+    const double dgn = __shfl(dg, lane < 63 ? lane + 1 : lane), sbn = __shfl(sb, lane < 63 ? lane + 1 : lane);
+    const double dgp = __shfl(dg, lane > 0 ? lane - 1 : 0);
+    const double yn = __shfl(y0, lane < 63 ? lane + 1 : lane), yp = __shfl(y0, lane > 0 ? lane - 1 : 0);
+    if (lane < p) {
+        const int kind = mypiv;
+        double out = 0.0;  // null pivot contributes 0
+        if (kind == PIV_1X1) {
+            out = y0 / dg;
+        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+            const bool first = kind == PIV_2X2_A;
+            const double a = first ? dg : dgp, b = first ? sbn : sb, e = first ? dgn : dg;
+            const double det = a * e - b * b;
+            const double yA = first ? y0 : yp, yB = first ? yn : y0;
+            out = first ? (e * yA - b * yB) / det : (a * yB - b * yA) / det;
+        }
+        *zdst = out;
+    }
+}
+
+__device__ __forceinline__ double bwd_compute_win2(const double* __restrict__ L, int64_t Lo, int m, int p, double* P, int win,
+                                                   int c0, const double* x, int mypiv) {
+    const int lane = threadIdx.x;
+    const bool tri = lane < p;
+    const bool live = tri && mypiv != PIV_NULL;
+    const unsigned long long liveM = __ballot(live);
+    const unsigned long long twoBM = __ballot(tri && mypiv == PIV_2X2_B);
+    double xj = tri ? x[lane] : 0.0;
+    int c1 = p, base = cstart(m, c0);
+    for (;;) {
+        const bool mine = lane >= c0 && lane < c1;
+        const double* pk = P + (pcol(m, mine ? lane : c0) - base);  // pk[i] = L(i, lane), i >= lane
+        double s0 = 0.0, s1 = 0.0;
+        for (int i0 = p; i0 < m; i0 += 8) {  // rectangle rows, 8 per chunk (pairs: s0 even, s1 odd offsets)
+            double lv[8], xv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                lv[u] = pk[i0 + u];  // rows >= m read in-bounds garbage (kSolveSlack), unused
+                xv[u] = x[i0 + u];
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                if (i0 + u < m) s0 += lv[u] * xv[u];  // uniform
+                if (i0 + u + 1 < m) s1 += lv[u + 1] * xv[u + 1];
+            }
+        }
+        if (live && mine) xj -= s0 + s1;
+        for (int kh = p - 1; kh >= c0; kh -= 8) {  // triangle steps k = kh .. kh - 7 (>= c0)
+            double lv[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) lv[u] = pk[max(kh - u, 0)];  // L(k, lane) for lane < k
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int k = kh - u;
+                if (k >= c0) {  // uniform
+                    const double xb = readlane_d(xj, k);
+                    const double xk = (liveM >> k) & 1 ? xb : 0.0;
+                    const int skip = (twoBM >> k) & 1 ? k - 1 : -1;
+                    const double t = xj - lv[u] * xk;
+                    xj = (live && mine && lane < k && lane != skip) ? t : xj;
+                }
+            }
+        }
+        if (c0 == 0) break;
+        c1 = c0;
+        c0 = bwd_chunk_begin(m, p, c1, win);
+        base = cstart(m, c0);
+        __syncthreads();
+        stage_panel<4>(L, Lo + base, cstart(m, c1) - base, P);
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): the window's loads are all consumed here
+        __syncthreads();
+    }
+    return xj;
+}
+
 // The walk keeps ONE FrontPre: once a front's prefetched data is consumed (staged into LDS, its
 // scalars copied), the next front's loads are issued into the same registers, so no register copy of
 // an in-flight load (which would wait for it) is needed across iterations.
@@ -2860,7 +2549,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         df_issue<true>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         const int mypiv = ipl[lane];
-        fwd_compute_win(A.L, Lo, m, p, P, D.win, k1, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
+        fwd_compute_win2(A.L, Lo, m, p, P, D.win, k1, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         pend = par;
         __syncthreads();  // LDS reused by the next front
@@ -2911,13 +2600,381 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         df_issue<false>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         const int mypiv = ipl[lane];
-        const double xj = bwd_compute_win(A.L, Lo, m, p, P, D.win, c0, x, mypiv);
+        const double xj = bwd_compute_win2(A.L, Lo, m, p, P, D.win, c0, x, mypiv);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (lane < p) st_sc1(D.xs + woff + lane, xj);
         pend = f;
         __syncthreads();
     }
     signal();
+}
+
+// ---- register-resident dataflow solve (round 4): the default dataflow kernels ----
+// Same walk, hand-offs (sc1 update vectors / solution values, arrival counters / done epochs) and per-lane
+// arithmetic as k_solve_{fwd,bwd}_df, with the pivot-step loops taken off LDS:
+//  forward (lane = row i): column k of L arrives by one coalesced load straight into register B[k - k0]
+//    (rows k..m-1 of the column are consecutive in the packed trapezoid), the pivot loop is unrolled over
+//    the registers, pivot kinds are wave-uniform ballot masks (scalar bit tests, no branch per step) and
+//    y_k is broadcast by readlane: a step is one readlane pair, one FMA and one select, no memory access.
+//    Rows >= 64 (m > 64) take the same column updates afterwards from the broadcast values (same order).
+//  backward (lane = column j): the panel is read in 8-row windows (rectangle rows ascending, then the
+//    triangle's rows descending), eight lanes per 64-byte column piece, all windows of the front in flight
+//    in registers at once; each window is written to an LDS tile T[r * ld + c] (ld = 2 mod 32: the
+//    writes of a 16-lane group hit 32 distinct banks, a row read by the 64 lanes is contiguous) and
+//    consumed as rows of L, the operands of the column-oriented dot products / updates of bwd_compute.
+//  Both walks issue the next front's loads before draining the finished front's stores, so a front in
+//  the bulk of the tree costs one memory round trip (plus one for its children's / ancestors' values).
+constexpr int kRgCols = 32;   // forward: columns of L per register round
+constexpr int kRgSlots = 32;  // backward: 8-row x 8-column window pieces per register round
+
+// base[rel] with rel clamped into [0, n): a uniform 64-bit base plus a 32-bit byte offset (one VGPR per
+// address: the loads use the scalar-base addressing form)
+__device__ __forceinline__ double ld_clamped(const double* base, int rel, int n) {
+    const uint32_t off = (uint32_t)min(max(rel, 0), n - 1) * 8u;
+    return *reinterpret_cast<const double*>(reinterpret_cast<const char*>(base) + off);
+}
+
+
+struct RgFwdIn {
+    int piv;                    // lane < p: pivot kind
+    double e0;                  // lane < p: right-hand side at the own pivots (xs)
+    int32_t fp0, fp1;           // pivoted positions of the analysis-order rows lane, lane + 64
+    int my_cm;
+    long long my_rmo, my_cxo;   // children's edge records (lane < children)
+    uint32_t dep;               // arrival counter as seen at issue time (sc1)
+    double dgl, sbl;            // L(lane, lane), L(lane, lane - 1): the diagonal blocks of D
+    double B[kRgCols];          // B[u] = L(lane, k0 + u)
+};
+
+// L(row0 + lane, k0 + u) -> B[u], u < kRgCols (indices clamped into the front's panel: lanes / columns
+// outside it read a harmless in-panel value that no step uses)
+__device__ __forceinline__ void rg_load_cols(const double* __restrict__ L, int64_t Lo, int m, int p, int k0, int row0,
+                                             double (&B)[kRgCols]) {
+    const int lane = threadIdx.x;
+    const int sz = p * m - ((p * (p - 1)) >> 1);
+    int cs = cstart(m, k0);
+#pragma unroll
+    for (int u = 0; u < kRgCols; ++u) {
+        const int k = k0 + u;
+        const int rel = cs + row0 + lane - k;
+        if (k < p) B[u] = ld_clamped(L + Lo, rel, sz);  // uniform: only the front's columns are loaded
+        cs += m - k;
+    }
+}
+
+__device__ __forceinline__ void rg_fwd_issue(const SolveArgs& A, const DfArgs& D, const FrontRec& r, RgFwdIn& q) {
+    const int lane = threadIdx.x;
+    const int m = r.m, p = r.p;
+    const int64_t ro = r.ro;
+    q.piv = lane < p ? (int)A.piv[ro + lane] : 0;
+    q.e0 = lane < p ? D.xs[r.woff + lane] : 0.0;
+    q.fp0 = lane < m ? A.fpos[ro + lane] : 0;
+    q.fp1 = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
+    q.my_cm = 0;
+    q.my_rmo = q.my_cxo = 0;
+    if (lane < r.c1 - r.c0) {
+        q.my_cm = A.ch_cm[r.c0 + lane];
+        q.my_rmo = A.ch_relmap_off[r.c0 + lane];
+        q.my_cxo = D.ch_cvx_off[r.c0 + lane];
+    }
+    q.dep = r.c1 > r.c0 ? ld_sc1_u32(D.cnt + r.f) : 0u;
+    const int lc = lane < p ? lane : 0;
+    q.dgl = A.L[r.Lo + cstart(m, lc)];
+    q.sbl = lane > 0 && lane < p ? A.L[r.Lo + cstart(m, lane - 1) + 1] : 0.0;
+    rg_load_cols(A.L, r.Lo, m, p, 0, 0, q.B);
+}
+
+// children's update vectors -> y (LDS rows, permuted by fpl), two children's loads in flight at a time
+// (the register-resident forward keeps its panel registers live here); rows 64.. of a child only when
+// the child has them.  Same additions, same order as fwd_extend_add.
+__device__ __forceinline__ void rg_extend_add(const SolveArgs& A, const DfArgs& D, int c0, int c1, int my_cm,
+                                              long long my_rmo, long long my_cxo, double* y, const int32_t* fpl) {
+    const int lane = threadIdx.x;
+    constexpr int CH = 2;
+    for (int cb = c0; cb < c1; cb += CH) {
+        if (cb != c0 && (cb - c0) % 64 == 0 && lane < c1 - cb) {  // more than 64 children: next records
+            my_cm = A.ch_cm[cb + lane];
+            my_rmo = A.ch_relmap_off[cb + lane];
+            my_cxo = D.ch_cvx_off[cb + lane];
+        }
+        double v[CH];
+        int32_t rw[CH];
+        int cms[CH];
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {
+            const int q = (cb - c0) % 64 + u;
+            const bool have = cb + u < c1;  // uniform
+            const int cm = have ? __builtin_amdgcn_readlane(my_cm, q) : 0;
+            cms[u] = cm;
+            const int32_t* rmp = A.relmap + (have ? (int64_t)readlane64((unsigned long long)my_rmo, q) : 0);
+            const double* cvp = D.cvx + (have ? (int64_t)readlane64((unsigned long long)my_cxo, q) : 0);
+            v[u] = lane < cm ? ld_sc1(cvp + lane) : 0.0;
+            rw[u] = lane < cm ? rmp[lane] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < CH; ++u) {  // children in order (rows of one child are distinct)
+            if (rw[u] >= 0) y[fpl[rw[u]]] += v[u];
+            if (cms[u] > 64) {  // uniform: the child's rows 64..
+                const int q = (cb - c0) % 64 + u;
+                const int32_t* rmp = A.relmap + (int64_t)readlane64((unsigned long long)my_rmo, q);
+                const double* cvp = D.cvx + (int64_t)readlane64((unsigned long long)my_cxo, q);
+                const int t = lane + 64;
+                if (t < cms[u]) y[fpl[rmp[t]]] += ld_sc1(cvp + t);
+            }
+        }
+    }
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_fwd_rg(SolveArgs A, DfArgs D) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    const int G = gridDim.x;
+    int t = blockIdx.x;
+    if (t >= D.nf) return;
+    double* y = smem_s;                         // 128 doubles: the front's rows (pivoted order)
+    int32_t* fpl = (int32_t*)(smem_s + 128);    // 128 words
+    FrontRec r = df_record(df_desc_load(D, t));
+    RgFwdIn q;
+    rg_fwd_issue(A, D, r, q);
+    int dn = df_desc_load(D, min(t + G, D.nf - 1));
+    for (;;) {
+        const int m = r.m, p = r.p, f = r.f, par = r.par;
+        unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f : nullptr;
+        if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long liveM = __ballot(lane < p && q.piv != PIV_NULL);
+        const unsigned long long twoAM = __ballot(lane < p && q.piv == PIV_2X2_A);
+        y[lane] = q.e0;
+        y[lane + 64] = 0.0;
+        fpl[lane] = q.fp0;
+        fpl[lane + 64] = q.fp1;
+        if (r.c1 > r.c0) {
+            const uint32_t target = D.epoch * (uint32_t)(r.c1 - r.c0);
+            if ((int32_t)(q.dep - target) < 0) df_wait(D.cnt + f, target, D.abort_flag);
+            rg_extend_add(A, D, r.c0, r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
+        }
+        double y0 = y[lane];
+        double a1 = m > 64 ? y[lane + 64] : 0.0;
+        if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+        // pivot steps on the rows < 64, columns in register rounds of kRgCols
+        for (int k0 = 0; k0 < p; k0 += kRgCols) {
+            if (k0 > 0) rg_load_cols(A.L, r.Lo, m, p, k0, 0, q.B);
+#pragma unroll
+            for (int u = 0; u < kRgCols; ++u) {
+                const int k = k0 + u;
+                if (k < p) {  // uniform
+                    const double yb = readlane_d(y0, k);
+                    const double yk = (liveM >> k) & 1 ? yb : 0.0;
+                    const int lim = (twoAM >> k) & 1 ? k + 1 : k;
+                    const double tv = y0 - q.B[u] * yk;
+                    y0 = lane > lim ? tv : y0;
+                }
+            }
+        }
+        // rows 64..m-1: the same column updates with the values the steps broadcast (y_k, 0 for a null pivot)
+        if (m > 64) {
+            const double ybv = lane < p && ((liveM >> lane) & 1) ? y0 : 0.0;
+            for (int k0 = 0; k0 < p; k0 += kRgCols) {
+                rg_load_cols(A.L, r.Lo, m, p, k0, 64, q.B);
+#pragma unroll
+                for (int u = 0; u < kRgCols; ++u) {
+                    const int k = k0 + u;
+                    if (k < p) a1 -= q.B[u] * readlane_d(ybv, k);
+                }
+            }
+        }
+        // update vector (rows >= p) and the own pivots' z = D^-1 y
+        double* cvo = D.cvx + r.xoff;
+        if (lane >= p && lane < m) st_sc1(cvo + (lane - p), y0);
+        if (lane + 64 < m) st_sc1(cvo + (lane + 64 - p), a1);
+        {
+            const double dg = q.dgl, sb = q.sbl;
+            const double dgn = __shfl(dg, lane < 63 ? lane + 1 : lane), sbn = __shfl(sb, lane < 63 ? lane + 1 : lane);
+            const double dgp = __shfl(dg, lane > 0 ? lane - 1 : 0);
+            const double yn = __shfl(y0, lane < 63 ? lane + 1 : lane), yp = __shfl(y0, lane > 0 ? lane - 1 : 0);
+            const int kind = q.piv;
+            double out = 0.0;  // null pivot contributes 0
+            if (kind == PIV_1X1) {
+                out = y0 / dg;
+            } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+                const bool first = kind == PIV_2X2_A;
+                const double a = first ? dg : dgp, b = first ? sbn : sb, e = first ? dgn : dg;
+                const double det = a * e - b * b;
+                const double yA = first ? y0 : yp, yB = first ? yn : y0;
+                out = first ? (e * yA - b * yB) / det : (a * yB - b * yA) / det;
+            }
+            if (lane < p) D.xs[r.woff + lane] = out;
+        }
+        if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+        // the next front's loads go out before this front's stores are drained
+        const int tn = t + G;
+        const bool more = tn < D.nf;
+        asm volatile("" ::: "memory");  // the next front's loads are not hoisted above this front's work
+        if (more) {
+            r = df_record(dn);
+            dn = df_desc_load(D, min(tn + G, D.nf - 1));
+            rg_fwd_issue(A, D, r, q);
+        }
+        drain_stores();
+        if (par >= 0 && lane == 0) __hip_atomic_fetch_add(D.cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+        if (!more) break;
+        t = tn;
+    }
+}
+
+// backward: window geometry of a front (OCT column octets per 8-row window)
+struct RgBwdIn {
+    int piv;          // lane < p: pivot kind
+    double e0;        // lane < p: z (forward result)
+    int32_t a0, a1;   // xs index of the rows lane, lane + 64 (>= p): the ancestors' solution values
+    uint32_t dep;     // parent's done word as seen at issue time (sc1)
+    double B[kRgSlots];
+};
+
+// windows: q < nr: rectangle rows [p + 8q, ..), else triangle rows [8t, ..), t = nt - 1 - (q - nr)
+__device__ __forceinline__ int rg_win_row(int m, int p, int q) {
+    const int nr = (m - p + 7) >> 3, nt = (p + 7) >> 3;
+    return q < nr ? p + 8 * q : 8 * (nt - 1 - (q - nr));
+}
+
+// Window pieces: a chunk is one window's columns [32 h, 32 h + 32) (h = 0, and h = 1 when p > 32), as four
+// 8 x 8 pieces; piece c of chunk g: lane l holds L(row0 + (l & 7), 32 h + 8 c + (l >> 3)).  One register
+// round holds kRgSlots / 4 = 8 chunks (fronts of C3: every window of the front).
+constexpr int kRgLd = 66;  // LDS row stride of a window tile (doubles, 2 mod 32)
+__device__ __forceinline__ void rg_load_windows(const double* __restrict__ L, int64_t Lo, int m, int p, int g0,
+                                                double (&B)[kRgSlots]) {
+    const int lane = threadIdx.x;
+    const int rr = lane & 7, kk = lane >> 3;
+    const int sz = p * m - ((p * (p - 1)) >> 1);
+    const int hs = p > 32 ? 1 : 0;
+#pragma unroll
+    for (int w = 0; w < kRgSlots / 4; ++w) {
+        const int g = g0 + w;
+        const int a = rg_win_row(m, p, g >> hs);
+        const int h = g & hs;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const int col = 32 * h + 8 * c + kk;
+            if (32 * h + 8 * c < p) B[w * 4 + c] = ld_clamped(L + Lo, cstart(m, col) + a + rr - col, sz);  // uniform
+        }
+    }
+}
+
+__device__ __forceinline__ void rg_bwd_issue(const SolveArgs& A, const DfArgs& D, const FrontRec& r, RgBwdIn& q) {
+    const int lane = threadIdx.x;
+    const int m = r.m, p = r.p;
+    const int64_t ro = r.ro;
+    q.piv = lane < p ? (int)A.piv[ro + lane] : (int)PIV_NULL;
+    q.e0 = lane < p ? D.xs[r.woff + lane] : 0.0;
+    q.a0 = lane < m && lane >= p ? D.rxpos[ro + lane] : 0;
+    q.a1 = lane + 64 < m ? D.rxpos[ro + lane + 64] : 0;
+    q.dep = r.par >= 0 ? ld_sc1_u32(D.done + r.par) : 0u;
+    rg_load_windows(A.L, r.Lo, m, p, 0, q.B);
+}
+
+// the windows of one front, lane = column j: rectangle dot products (two accumulators by row parity, as
+// bwd_compute), then the triangle's rows descending; x (LDS) holds the rows' values, T one window
+__device__ __forceinline__ double rg_bwd_front(const SolveArgs& A, const FrontRec& r, RgBwdIn& q, unsigned long long liveM,
+                                               unsigned long long twoBM, double xr0, double xr1, double* T, double xj) {
+    const int lane = threadIdx.x;
+    const int m = r.m, p = r.p;
+    constexpr int ld = kRgLd;
+    constexpr int NG = kRgSlots / 4;
+    const int rr = lane & 7, kk = lane >> 3;
+    const int nr = (m - p + 7) >> 3, nt = (p + 7) >> 3;
+    const int hs = p > 32 ? 1 : 0;
+    const int nchunk = (nr + nt) << hs;
+    const bool live = lane < p && q.piv != PIV_NULL;
+    double s0 = 0.0, s1 = 0.0;
+    for (int g0 = 0; g0 < nchunk; g0 += NG) {
+        if (g0 > 0) rg_load_windows(A.L, r.Lo, m, p, g0, q.B);
+#pragma unroll
+        for (int w = 0; w < NG; ++w) {
+            const int g = g0 + w;
+            if (g >= nchunk) continue;  // uniform
+            const int h = g & hs;
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (32 * h + 8 * c < p) T[rr * ld + 32 * h + 8 * c + kk] = q.B[w * 4 + c];  // uniform
+            if (h != hs) continue;  // the window's second column chunk is still to come
+            const int qw = g >> hs;
+            if (qw < nr) {  // rectangle rows a .. a + 7 (< m), ascending
+                const int a = p + 8 * qw;
+#pragma unroll
+                for (int u = 0; u < 8; u += 2) {  // x_i broadcast from the lane holding row i
+                    if (a + u < m) {
+                        const int i = a + u;
+                        const double xv = i < 64 ? readlane_d(xr0, i) : readlane_d(xr1, i - 64);
+                        s0 += T[u * ld + lane] * xv;
+                    }
+                    if (a + u + 1 < m) {
+                        const int i = a + u + 1;
+                        const double xv = i < 64 ? readlane_d(xr0, i) : readlane_d(xr1, i - 64);
+                        s1 += T[(u + 1) * ld + lane] * xv;
+                    }
+                }
+                if (qw == nr - 1 && live) xj -= s0 + s1;
+            } else {  // triangle rows k = b - 1 .. a
+                if (qw == 0 && live) xj -= s0 + s1;  // no rectangle rows
+                const int a = 8 * (nt - 1 - (qw - nr));
+                const int b = min(a + 8, p);
+#pragma unroll
+                for (int u = 7; u >= 0; --u) {
+                    const int k = a + u;
+                    if (k < b) {
+                        const double l = T[u * ld + lane];
+                        const double xb = readlane_d(xj, k);
+                        const double xk = (liveM >> k) & 1 ? xb : 0.0;
+                        const int skip = (twoBM >> k) & 1 ? k - 1 : -1;
+                        const double tv = xj - l * xk;
+                        xj = (live && lane < k && lane != skip) ? tv : xj;
+                    }
+                }
+            }
+        }
+    }
+    return xj;
+}
+
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_bwd_rg(SolveArgs A, DfArgs D) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    const int G = gridDim.x;
+    int t = blockIdx.x;
+    if (t >= D.nf) return;
+    double* T = smem_s;         // one 8-row window of L (8 x ld doubles)
+    FrontRec r = df_record(df_desc_load(D, D.nf - 1 - t));
+    RgBwdIn q;
+    rg_bwd_issue(A, D, r, q);
+    int dn = df_desc_load(D, D.nf - 1 - min(t + G, D.nf - 1));
+    for (;;) {
+        const int m = r.m, p = r.p, f = r.f;
+        unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f + 4 : nullptr;
+        if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
+        const unsigned long long liveM = __ballot(lane < p && q.piv != PIV_NULL);
+        const unsigned long long twoBM = __ballot(lane < p && q.piv == PIV_2X2_B);
+        if (r.par >= 0 && (int32_t)(q.dep - D.epoch) < 0) df_wait(D.done + r.par, D.epoch, D.abort_flag);
+        // the rows' values in lane = row order: own z (lane < p), the ancestors' published solution values
+        const double xr0 = lane < p ? q.e0 : (lane < m ? ld_sc1(D.xs + q.a0) : 0.0);
+        const double xr1 = lane + 64 < m ? ld_sc1(D.xs + q.a1) : 0.0;
+        if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
+        const double xj = rg_bwd_front(A, r, q, liveM, twoBM, xr0, xr1, T, q.e0);
+        if (lane < p) st_sc1(D.xs + r.woff + lane, xj);
+        if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+        const int tn = t + G;
+        const bool more = tn < D.nf;
+        asm volatile("" ::: "memory");  // the next front's loads are not hoisted above this front's work
+        if (more) {
+            r = df_record(dn);
+            dn = df_desc_load(D, D.nf - 1 - min(tn + G, D.nf - 1));
+            rg_bwd_issue(A, D, r, q);
+        }
+        drain_stores();
+        if (lane == 0) __hip_atomic_store(D.done + f, D.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
+        if (!more) break;
+        t = tn;
+    }
 }
 
 // right-hand side into elimination order (xs[xpos[i]] = s_i b_i) and the solution back (x_i = s_i xs[xpos[i]])
@@ -3077,508 +3134,6 @@ __global__ __launch_bounds__(kThreads) void k_big_child(FactorArgs A, const int3
     }
 }
 
-__global__ __launch_bounds__(kThreads) void k_big_panel(FactorArgs A, const int32_t* __restrict__ fronts) {
-    extern __shared__ __attribute__((aligned(16))) double colbuf[];  // column k brought up to date (m doubles)
-    __shared__ double wk[kBigNB + 2], cA[kBigNB + 2], cB[kBigNB + 2], red[4];
-    __shared__ int bq[kBigNB + 2];
-    __shared__ BigFrontState S;
-    __shared__ FrontShared sh;
-    const int tid = threadIdx.x;
-    const int f = fronts[blockIdx.x];
-    if (tid == 0) S = A.big[f];
-    __syncthreads();
-    if (S.done) {  // the last panel's update has been applied: nothing pending for k_big_update
-        if (tid == 0 && S.k1 != S.k0) { A.big[f].k0 = S.k1; }
-        return;
-    }
-    if (A.big_app && !S.exact) return;  // the a-posteriori step is in charge (k_app_*)
-    const int m = A.fm[f], p = A.fp[f];
-    const int64_t ro = A.rows_off[f];
-    const FullStore st{A.gscratch + A.gscratch_off[f], m};
-    int32_t* lrow = A.frow + ro;
-    int32_t* lorig = A.fpos + ro;
-    int8_t* piv = A.piv + ro;
-    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
-    double minpiv = S.minpiv;  // wave 0 keeps it (uniform)
-    const int k0 = S.k;
-    int k = k0;
-    while (k < p && k - k0 < kBigNB) {
-        const int np = k - k0;
-        // left-looking: column k minus the panel's pivots, into colbuf (the store keeps the stale column
-        // until the pivot is accepted: a panel that stops here leaves it to k_big_update)
-        for (int q = tid; q < np; q += kThreads) wk[q] = st.at(k, k0 + q);
-        __syncthreads();
-        for (int i = k + tid; i < m; i += kThreads) {
-            double acc = st.at(i, k);
-            for (int q = 0; q < np; ++q) {
-                double l = cA[q] * st.at(i, bq[q]);
-                if (cB[q] != 0.0) l += cB[q] * st.at(i, bq[q] + 1);
-                acc -= l * wk[q];
-            }
-            colbuf[i] = acc;
-        }
-        __syncthreads();
-        const double akk = colbuf[k];
-        double g = 0.0;
-        for (int i = k + 1 + tid; i < m; i += kThreads) g = fmax(g, fabs(colbuf[i]));
-        g = block_max256(g, red);
-        const double aak = fabs(akk);
-        if (aak > thres && !(A.u * g > aak)) {  // 1x1 pivot at k without interchange (quick test)
-            for (int i = k + tid; i < m; i += kThreads) st.at(i, k) = colbuf[i];
-            if (tid == 0) {
-                piv[k] = PIV_1X1;
-                if (akk > 0.0) S.npos++; else S.nneg++;
-                cA[np] = 1.0 / akk; cB[np] = 0.0; bq[np] = k;
-            }
-            minpiv = fmin(minpiv, aak);
-            __syncthreads();
-            k += 1;
-            continue;
-        }
-        if (np > 0) break;  // the trailing update must land before a full search
-        // panel start: every column is current -> the exact search of the small-front kernels
-        if (tid < 64) {
-            const PivotDecision d = search_pivot(st, m, k, p, A.u, thres, minpiv);
-            if (tid == 0) sh.dec = d;
-        }
-        __syncthreads();
-        PivotDecision d = sh.dec;
-        if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
-        if (d.c != k) {
-            sym_swap<kThreads>(st, m, k, d.c, lrow, lorig);
-            __syncthreads();
-        }
-        if (d.kind == PIV_2X2_A) {
-            const int r = d.r == k ? d.c : d.r;
-            if (r != k + 1) {
-                sym_swap<kThreads>(st, m, k + 1, r, lrow, lorig);
-                __syncthreads();
-            }
-        }
-        if (tid == 0) {
-            if (sh.dec.kind == PIV_STUCK) S.nstuck++;
-            S.nrel += d.relaxed;
-            if (d.relaxed && !S.delays && A.record_delays && A.fparent[f] >= 0) {  // see factor_front
-                S.delays = 1;
-                const unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
-                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
-            }
-        }
-        if (d.kind == PIV_NULL) {
-            for (int i = k + 1 + tid; i < m; i += kThreads) st.at(i, k) = 0.0;
-            if (tid == 0) { piv[k] = PIV_NULL; S.nzero++; cA[0] = 0.0; cB[0] = 0.0; bq[0] = k; }
-            __syncthreads();
-            k += 1;
-        } else if (d.kind == PIV_1X1) {
-            if (tid == 0) {
-                const double dk = st.at(k, k);
-                piv[k] = PIV_1X1;
-                if (dk > 0.0) S.npos++; else S.nneg++;
-                cA[0] = 1.0 / dk; cB[0] = 0.0; bq[0] = k;
-            }
-            __syncthreads();
-            k += 1;
-        } else {  // 2x2 on (k, k+1)
-            if (tid == 0) {
-                const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
-                const double det = a * e - b * b, idet = 1.0 / det;
-                piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; S.n2++;
-                if (det < 0.0) { S.npos++; S.nneg++; }
-                else if (a + e > 0.0) S.npos += 2;
-                else S.nneg += 2;
-                cA[0] = e * idet; cB[0] = -b * idet; bq[0] = k;
-                cA[1] = -b * idet; cB[1] = a * idet; bq[1] = k;
-            }
-            __syncthreads();
-            k += 2;
-        }
-    }
-    if (tid == 0) {
-        S.minpiv = minpiv;
-        S.k0 = k0;
-        S.k1 = k;
-        S.k = k;
-        S.done = k >= p;
-        S.exact = 0;
-        A.big[f] = S;
-    }
-}
-
-// Register-resident panel (fronts of m <= 256 * S; k_big_panel above stays for larger ones).  The
-// column-at-a-time left-looking loop of k_big_panel re-reads the panel's earlier columns from HBM for
-// every pivot (m * np scattered loads per step, ~40 us per pivot at m = 2048).  Here the panel rows
-// [k0, m) x columns [k0, k0 + NB) are loaded ONCE into registers -- thread t owns rows k0 + t + 256 s,
-// each row's NB columns one contiguous run of the row-major front -- and eliminated right-looking: per
-// pivot step the column's largest sub-diagonal magnitude (wave max tree + one workgroup barrier; the
-// diagonal block's column values through LDS, double-buffered by step parity so one barrier per step
-// suffices), the quick Duff-Reid 1x1 test of k_big_panel, then NB - c - 1 FMAs per owned row.  The
-// products are the left-looking ones of k_big_panel in the same order per element (L(i,q) = W(i,q) / d_q
-// times W(j,q), pivots q ascending), so the pivot sequence and counters follow the same rule.  A failure
-// at the panel's first column takes k_big_panel's exact search on the front in HBM (interchanges, 2x2,
-// null pivots, relaxation ladder, delays); its one or two pivots are applied to the reloaded register
-// panel (left-looking terms) and the panel continues.  A failure later ends the panel.  Only pivoted
-// columns are written back (un-normalised W, as k_big_panel stores them); the trailing columns stay
-// stale in HBM for k_big_update.
-template <int S, int NB, int T, bool SEARCH = true>
-__global__ __launch_bounds__(T) __attribute__((amdgpu_waves_per_eu(T / 256, T / 256))) void k_big_panel_reg(FactorArgs A, const int32_t* __restrict__ fronts) {
-    __shared__ double colk[2][NB], red[2][T / 64];
-    __shared__ double cA[4], cB[4];
-    __shared__ int bq[4];
-    __shared__ double rowK[NB], rowC[NB], colX[NB], sred[T / 64];  // in-panel search / interchange
-    __shared__ unsigned long long ured[T / 64];
-    __shared__ BigFrontState SF;
-    __shared__ FrontShared sh;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int f = fronts[blockIdx.x];
-    if (tid == 0) SF = A.big[f];
-    __syncthreads();
-    if (SF.done) {  // the last panel's update has been applied: nothing pending for k_big_update
-        if (tid == 0 && SF.k1 != SF.k0) { A.big[f].k0 = SF.k1; }
-        return;
-    }
-    if (A.big_app && !SF.exact) return;  // the a-posteriori step is in charge (k_app_*)
-    const int m = A.fm[f], p = A.fp[f];
-    const int64_t ro = A.rows_off[f];
-    const FullStore st{A.gscratch + A.gscratch_off[f], m};
-    int32_t* lrow = A.frow + ro;
-    int32_t* lorig = A.fpos + ro;
-    int8_t* piv = A.piv + ro;
-    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
-    double minpiv = SF.minpiv;  // uniform
-    const int k0 = SF.k;
-    const int ncol = min(NB, p - k0);  // fully-summed columns of this panel
-    // diagnostics (option stamps = 6): s_memrealtime ticks per phase summed into stamps[8 f + phase]
-    const bool stamp = A.stamps != nullptr && A.stamp_mode == 6 && tid == 0;
-    unsigned long long t_last = stamp ? __builtin_amdgcn_s_memrealtime() : 0ull;
-    auto tick = [&](int ph) __attribute__((always_inline)) {
-        if (stamp) {
-            const unsigned long long t = __builtin_amdgcn_s_memrealtime();
-            atomicAdd(&A.stamps[8 * (int64_t)f + ph], t - t_last);
-            t_last = t;
-        }
-    };
-    // one vector register tuple per owned row: static columns in the pivot steps, dynamic (uniform) ones in
-    // the in-panel search via indexed register moves -- never scratch
-    typedef double RowV __attribute__((ext_vector_type(NB)));
-    typedef double RowA[NB];
-    typename std::conditional<SEARCH, RowV, RowA>::type P[S];
-    auto load = [&]() __attribute__((always_inline)) {
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int r = k0 + tid + T * s;
-            const double* row = st.F + (int64_t)(r < m ? r : k0) * m + k0;
-#pragma unroll
-            for (int c = 0; c < NB; ++c) P[s][c] = (r < m && k0 + c < m) ? row[c] : 0.0;
-        }
-    };
-    // right-looking quick-test steps from register column cstart; returns the column where the panel stops
-    auto steps = [&](int cstart) __attribute__((always_inline)) -> int {
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
-            if (c < cstart) continue;
-            if (c >= ncol) break;  // uniform
-            const int buf = c & 1;
-            double mx = 0.0;
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const int r = k0 + tid + T * s;
-                mx = (r > k0 + c && r < m) ? fmax(mx, fabs(P[s][c])) : mx;
-            }
-            if (tid >= c && tid < NB) colk[buf][tid] = P[0][c];  // A(k0 + tid, k0 + c), diagonal block
-            mx = wave_max_abs(mx);
-            if (lane == 0) red[buf][wv] = mx;
-            __syncthreads();
-            double g = red[buf][0];
-#pragma unroll
-            for (int w = 1; w < T / 64; ++w) g = fmax(g, red[buf][w]);
-            const double akk = colk[buf][c];
-            const double aak = fabs(akk);
-            if (!(aak > thres) || A.u * g > aak) return c;  // uniform: the quick 1x1 test failed
-            const double dinv = 1.0 / akk;
-            minpiv = fmin(minpiv, aak);
-            double l[S];
-#pragma unroll
-            for (int s = 0; s < S; ++s) l[s] = P[s][c] * dinv;
-#pragma unroll
-            for (int j = c + 1; j < NB; ++j) {  // column operand from LDS (broadcast), one at a time
-                const double wj = colk[buf][j];
-#pragma unroll
-                for (int s = 0; s < S; ++s) P[s][j] -= l[s] * wj;
-            }
-            if (tid == 0) {  // pivot kinds are stored after the loop (a global store here would be waited for
-                             // by the next step's barrier)
-                if (akk > 0.0) SF.npos++; else SF.nneg++;
-            }
-        }
-        return ncol;
-    };
-    // quick 1x1 test of the panel's first column, current in HBM at the panel start; on a failure the
-    // exact search of the small-front kernels decides the first pivot(s) before the registers are loaded
-    int np = 0;  // pivots of the exact search (0, 1 or 2)
-    bool full = false;
-    if (ncol > 0) {
-        double g0 = 0.0;
-#pragma unroll 8
-        for (int i = k0 + 1 + tid; i < m; i += T) g0 = fmax(g0, fabs(st.at(i, k0)));
-        g0 = wave_max_abs(g0);
-        if (lane == 0) red[0][wv] = g0;
-        __syncthreads();
-        g0 = red[0][0];
-#pragma unroll
-        for (int w = 1; w < T / 64; ++w) g0 = fmax(g0, red[0][w]);
-        __syncthreads();
-        const double a0 = fabs(st.at(k0, k0));
-        full = !(a0 > thres) || A.u * g0 > a0;
-    }
-    if (full) {
-        const int k = k0;
-        {
-            const PivotDecision d = search_pivot_blk<T>(st, m, k, p, A.u, thres, minpiv, ured);
-            if (tid == 0) sh.dec = d;
-        }
-        __syncthreads();
-        PivotDecision d = sh.dec;
-        if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
-        if (d.c != k) {
-            sym_swap_batched<T>(st, m, k, d.c, lrow, lorig);
-            __syncthreads();
-        }
-        if (d.kind == PIV_2X2_A) {
-            const int r = d.r == k ? d.c : d.r;
-            if (r != k + 1) {
-                sym_swap_batched<T>(st, m, k + 1, r, lrow, lorig);
-                __syncthreads();
-            }
-        }
-        if (tid == 0) {
-            if (sh.dec.kind == PIV_STUCK) SF.nstuck++;
-            SF.nrel += d.relaxed;
-            if (d.relaxed && !SF.delays && A.record_delays && A.fparent[f] >= 0) {  // see factor_front
-                SF.delays = 1;
-                const unsigned long long base = atomicAdd(&A.counters[6], (unsigned long long)(p - k));
-                for (int q = k; q < p; ++q) A.delayed[base + (q - k)] = lrow[q];
-            }
-        }
-        if (d.kind == PIV_NULL) {
-            for (int i = k + 1 + tid; i < m; i += T) st.at(i, k) = 0.0;
-            if (tid == 0) { piv[k] = PIV_NULL; SF.nzero++; cA[0] = 0.0; cB[0] = 0.0; bq[0] = k; }
-            np = 1;
-        } else if (d.kind == PIV_1X1) {
-            if (tid == 0) {
-                const double dk = st.at(k, k);
-                piv[k] = PIV_1X1;
-                if (dk > 0.0) SF.npos++; else SF.nneg++;
-                cA[0] = 1.0 / dk; cB[0] = 0.0; bq[0] = k;
-            }
-            np = 1;
-        } else {  // 2x2 on (k, k+1)
-            if (tid == 0) {
-                const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
-                const double det = a * e - b * b, idet = 1.0 / det;
-                piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; SF.n2++;
-                if (det < 0.0) { SF.npos++; SF.nneg++; }
-                else if (a + e > 0.0) SF.npos += 2;
-                else SF.nneg += 2;
-                cA[0] = e * idet; cB[0] = -b * idet; bq[0] = k;
-                cA[1] = -b * idet; cB[1] = a * idet; bq[1] = k;
-            }
-            np = 2;
-        }
-        __syncthreads();
-    }
-    tick(0);  // quick test of the first column (+ exact search, interchanges)
-    load();
-    // the interchanged front minus the exact-search pivots' terms on the panel's later columns
-    for (int q = 0; q < np; ++q) {
-        const double ca = cA[q], cb = cB[q];
-        const int b0 = bq[q];
-        double lq[S];
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int r = k0 + tid + T * s;
-            double l = 0.0;
-            if (r < m) {
-                l = ca * st.at(r, b0);
-                if (cb != 0.0) l += cb * st.at(r, b0 + 1);
-            }
-            lq[s] = l;
-        }
-#pragma unroll
-        for (int j = 1; j < NB; ++j) {
-            if (j < np || k0 + j >= m) continue;
-            const double wj = st.at(k0 + j, k0 + q);  // W(j, q): row k0 + j > column k0 + q
-#pragma unroll
-            for (int s = 0; s < S; ++s) P[s][j] -= lq[s] * wj;
-        }
-    }
-    const int cw0 = np;  // first register column to write back
-    // ---- exact search restricted to the panel ----
-    // At a column c whose quick test fails, the exact rule (search_pivot, first threshold level) examines
-    // the candidates c, c+1, ... in order.  The panel's columns are current for every row, so as long as
-    // the candidates lie in the panel the same tests are evaluated here; a 1x1 acceptance is applied by a
-    // symmetric interchange in the registers (+ the rows' earlier columns in HBM) and the panel goes on.
-    // Anything else -- a null pivot, a 2x2 the rule would take, a 2x2 partner outside the panel, no
-    // candidate left in the panel -- ends the call; the exact search then runs on the updated front.
-    auto pget = [&](int s, int j) __attribute__((always_inline)) -> double { return P[s][j]; };
-    auto bmax = [&](double v) __attribute__((always_inline)) -> double {  // non-negative values
-        v = wave_max_abs(v);
-        if (lane == 0) sred[wv] = v;
-        __syncthreads();
-        double r = sred[0];
-#pragma unroll
-        for (int w = 1; w < T / 64; ++w) r = fmax(r, sred[w]);
-        __syncthreads();
-        return r;
-    };
-    auto bmaxu = [&](unsigned long long v) __attribute__((always_inline)) -> unsigned long long {
-        v = wave_max_u64(v);
-        if (lane == 0) ured[wv] = v;
-        __syncthreads();
-        unsigned long long r = ured[0];
-#pragma unroll
-        for (int w = 1; w < T / 64; ++w) r = umax64(r, ured[w]);
-        __syncthreads();
-        return r;
-    };
-    // max |A(i, col j)| over rows i >= k0 + c, i not in {k0 + j, k0 + x}: rows below from the column,
-    // rows in [k0 + c, k0 + j) from row k0 + j (upper triangle by symmetry)
-    auto colmax = [&](int c, int j, int x) __attribute__((always_inline)) -> double {
-        double g = 0.0;
-#pragma unroll
-        for (int s = 0; s < S; ++s) {
-            const int r = k0 + tid + T * s;
-            const double v = fabs(pget(s, j));
-            if (r > k0 + j && r < m && r != k0 + x) g = fmax(g, v);
-        }
-        if (tid == j)
-            for (int i = c; i < j; ++i)
-                if (i != x) g = fmax(g, fabs(pget(0, i)));
-        return bmax(g);
-    };
-    auto search = [&](int c) __attribute__((always_inline)) -> bool {
-        const int k = k0 + c;
-        for (int j = c; j < ncol; ++j) {
-            const int cand = k0 + j;
-            if (tid == j) colX[0] = pget(0, j);  // A(cand, cand)
-            const double g = colmax(c, j, -1);   // (barriers inside)
-            const double ajj = colX[0], acc = fabs(ajj);
-            if (fmax(acc, g) <= thres) return false;  // null pivot: the exact search decides
-            minpiv = fmin(minpiv, fmax(acc, g));
-            if (acc != 0.0 && acc >= A.u * g) {
-                if (j == c) return true;
-                // symmetric interchange of rows / columns k and cand (sym_swap in the register layout)
-                if (tid == c) for (int q = 0; q < NB; ++q) rowK[q] = pget(0, q);
-                if (tid == j) for (int q = 0; q < NB; ++q) rowC[q] = pget(0, q);
-                if (tid > c && tid < j) colX[tid] = pget(0, c);
-                __syncthreads();
-#pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    const int r = k0 + tid + T * s;
-                    if (r > cand && r < m) {  // rows below both: the two columns trade places
-                        const double vc = pget(s, c), vj = pget(s, j);
-#pragma unroll
-                        for (int jj = 0; jj < NB; ++jj) P[s][jj] = jj == c ? vj : (jj == j ? vc : P[s][jj]);
-                    }
-                }
-                if (tid == c) {  // row k <- row cand: columns < c, and the diagonal
-#pragma unroll
-                    for (int jj = 0; jj < NB; ++jj) P[0][jj] = jj < c ? rowC[jj] : (jj == c ? rowC[j] : P[0][jj]);
-                } else if (tid == j) {  // row cand <- row k: columns < c, (k, cand) rows' column k, diagonal
-#pragma unroll
-                    for (int jj = 0; jj < NB; ++jj)
-                        P[0][jj] = jj < c ? rowK[jj] : (jj > c && jj < j ? colX[jj] : (jj == j ? rowK[c] : P[0][jj]));
-                } else if (tid > c && tid < j) {  // A(i, k) <- A(cand, i)
-#pragma unroll
-                    for (int jj = 0; jj < NB; ++jj) P[0][jj] = jj == c ? rowC[tid] : P[0][jj];
-                }
-                // the two rows in the columns before the registers' write-back range, row ids
-                for (int q = tid; q < k0 + cw0; q += T) {
-                    const double a = st.F[(int64_t)k * m + q], b = st.F[(int64_t)cand * m + q];
-                    st.F[(int64_t)k * m + q] = b;
-                    st.F[(int64_t)cand * m + q] = a;
-                }
-                if (tid == 0) {
-                    int32_t y = lrow[k]; lrow[k] = lrow[cand]; lrow[cand] = y;
-                    y = lorig[k]; lorig[k] = lorig[cand]; lorig[cand] = y;
-                }
-                __syncthreads();
-                return true;
-            }
-            // 1x1 rejected: the largest off-diagonal among the fully-summed rows is the 2x2 partner
-            unsigned long long best = 0;
-            int bi = 0x7fffffff;
-            if (tid == j)
-                for (int i = c; i < j; ++i) {
-                    const unsigned long long b = as_bits(fabs(pget(0, i)));
-                    if (b > best) { best = b; bi = k0 + i; }
-                }
-#pragma unroll
-            for (int s = 0; s < S; ++s) {
-                const int r = k0 + tid + T * s;
-                if (r > cand && r < p && r < m) {
-                    const unsigned long long b = as_bits(fabs(pget(s, j)));
-                    if (b > best) { best = b; bi = r; }
-                }
-            }
-            const unsigned long long mx = bmaxu(best);
-            if (mx == 0) continue;
-            const unsigned long long ik = bmaxu(best == mx ? 0xffffffffull - (unsigned)bi : 0ull);
-            const int r = (int)(0xffffffffull - ik);
-            const int jr = r - k0;
-            if (jr >= ncol) return false;  // partner column outside the panel
-            const double gc = colmax(c, j, jr), gr = colmax(c, jr, j);
-            if (tid == jr) { colX[1] = pget(0, jr); if (r > cand) colX[2] = pget(0, j); }
-            if (tid == j && r < cand) colX[2] = pget(0, jr);
-            __syncthreads();
-            const double a = ajj, b = colX[2], e = colX[1];
-            __syncthreads();
-            const double det = a * e - b * b;
-            if (det != 0.0) {
-                const double lim = fabs(det) / A.u;
-                if (fabs(e) * gc + fabs(b) * gr <= lim && fabs(b) * gc + fabs(a) * gr <= lim) return false;  // 2x2
-            }
-        }
-        return false;
-    };
-    tick(1);  // register panel loaded, exact pivots' terms applied
-    int cend = np;
-    for (;;) {  // one call site each: the panel stays in registers
-        cend = steps(cend);
-        if constexpr (SEARCH) {
-            if (cend >= ncol || !search(cend)) break;
-        } else {
-            break;
-        }
-    }
-    tick(2);  // quick steps
-    // the panel back to the front (lower part, un-normalised): pivoted columns and the panel's later
-    // columns (current: the trailing update starts after the panel, at k0 + NB)
-#pragma unroll
-    for (int s = 0; s < S; ++s) {
-        const int r = k0 + tid + T * s;
-        if (r >= m) continue;
-        double* row = st.F + (int64_t)r * m + k0;
-#pragma unroll
-        for (int c = 0; c < NB; ++c)
-            if (c >= cw0 && r >= k0 + c) row[c] = P[s][c];
-    }
-    for (int c = cw0 + tid; c < cend; c += T) piv[k0 + c] = PIV_1X1;
-    const int k = k0 + cend;
-    __syncthreads();  // counters of thread 0 complete
-    if (tid == 0) {
-        SF.minpiv = minpiv;
-        SF.k0 = k0;
-        SF.k1 = k;
-        SF.k = k;
-        SF.done = k >= p;
-        SF.exact = 0;
-        SF.pad = min(k0 + NB, m);  // first row / column of the trailing update (the panel is current)
-        A.big[f] = SF;
-    }
-    tick(3);  // write-back
-    if (stamp) atomicAdd(&A.stamps[8 * (int64_t)f + 4], 1ull);
-}
-
 // Trailing update of the pending panel [k0, k1): rows / columns [k1, m), lower triangle.  Block = one
 // 64 x 64 macro tile (blockIdx.x, lower-triangular order) of front fronts[blockIdx.y]; wave w owns rows
 // 16w .. 16w+15 of it and four 16 x 16 MFMA accumulators along the columns.
@@ -3648,7 +3203,7 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
     }
 }
 
-// ---- a-posteriori blocked steps (FactorArgs::big_app) ----
+// ---- a-posteriori blocked steps of the large fronts ----
 // One step takes the next kAppNB columns of every unfinished large front in three launches, so the trailing
 // matrix is read and written once per kAppNB pivots (one rank-kAppNB MFMA update) instead of once per
 // register panel of 8 or 16:
@@ -4158,8 +3713,6 @@ static hipError_t launch_rowscanR(const ScanArgs& A, hipStream_t s) {
 hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
     if (A0.n == 0) return hipSuccess;
     SweepArgs A = A0;
-    static const int noatomic = getenv("UNO_KKT_SWEEP_NOATOMIC") ? 1 : 0;  // diagnostics (wrong scaling)
-    A.diag_noatomic = noatomic;
     const size_t sh = 16 * (size_t)std::max(A.max_m, 1);
     const dim3 gn(grid_for(A.n, 256));
     hipError_t e = A.rmax_zero ? hipSuccess : hipMemsetAsync(A.rmax, 0, sizeof(unsigned long long) * A.n, s);
@@ -4247,28 +3800,15 @@ size_t factor_lds_bytes(int mmax) {
            (size_t)((mmax + 15) & ~15) + (size_t)grid_rows * sizeof(double);
 }
 
-size_t factor_lds_bytes_mf(int mmax) {
-    return 32 + (size_t)mf_front_doubles(mmax) * sizeof(double) + 2 * (size_t)mmax * sizeof(double) +
-           2 * (size_t)mmax * sizeof(int32_t) + (size_t)((mmax + 15) & ~15);
-}
-
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s) {
     if (count <= 0) return hipSuccess;
     if (global) {
         return hipErrorInvalidValue;  // fronts beyond LDS: launch_big_* (host loop in kkt_api.cpp)
     } else {
-        static const size_t lpad = getenv("UNO_KKT_LDS_PAD_LDS") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD_LDS")) : 0;  // diagnostics
-        size_t sh = factor_lds_bytes(mmax) + lpad;
+        const size_t sh = factor_lds_bytes(mmax);
         // small fronts: one wave per front (no cross-wave barriers, more fronts per CU);
         // larger fronts: four waves on a 16x16 update grid
-        if (A.mf && mmax <= 64) {  // tile kernels (matrix-core trailing updates)
-            sh = factor_lds_bytes_mf(mmax);
-            static const size_t pad = getenv("UNO_KKT_LDS_PAD") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD")) : 0;  // diagnostics
-            sh += pad;
-            if (mmax <= 32) hipLaunchKernelGGL((k_factor_mf<2>), dim3(count), dim3(64), sh, s, A, fronts);
-            else hipLaunchKernelGGL((k_factor_mf<4>), dim3(count), dim3(64), sh, s, A, fronts);
-        } else if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
-        else if (mmax <= 64 && A.wpe2) hipLaunchKernelGGL((k_factor_lds<64, 8, 2>), dim3(count), dim3(64), sh, s, A, fronts);
+        if (mmax <= 32) hipLaunchKernelGGL((k_factor_lds<64, 4>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= 64) hipLaunchKernelGGL((k_factor_lds<64, 8>), dim3(count), dim3(64), sh, s, A, fronts);
         else if (mmax <= kMaxWaveFront) hipLaunchKernelGGL((k_factor_lds<64, 9>), dim3(count), dim3(64), sh, s, A, fronts);
         else hipLaunchKernelGGL((k_factor_lds<kThreads, 8>), dim3(count), dim3(kThreads), sh, s, A, fronts);
@@ -4394,28 +3934,12 @@ hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int c
 
 hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s) {
     if (count <= 0) return hipSuccess;
-    if (A.big_app) {
-        const int rb = (mmax + 63) / 64;
-        hipLaunchKernelGGL(k_app_diag, dim3(count), dim3(64), 0, s, A, fronts);
-        hipLaunchKernelGGL(k_app_rows, dim3(rb, count), dim3(256), 0, s, A, fronts);
-        hipLaunchKernelGGL(k_app_update, dim3(rb * (rb + 1) / 2 + rb, count), dim3(kThreads), 0, s, A, fronts, rb * (rb + 1) / 2);
-        static const bool panel_exact = getenv("UNO_KKT_APP_PANEL") != nullptr;  // A/B: the register panel instead
-        if (!panel_exact) {
-            hipLaunchKernelGGL(k_app_exact, dim3(count), dim3(512), 0, s, A, fronts);
-            const int nt = (mmax + 63) / 64;
-            hipLaunchKernelGGL(k_big_update, dim3(nt * (nt + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
-            return hipGetLastError();
-        }
-    }
-    static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;  // diagnostics: the left-looking panel
-    if (legacy || mmax > 16 * kThreads) hipLaunchKernelGGL(k_big_panel, dim3(count), dim3(kThreads), (size_t)mmax * sizeof(double) + 16, s, A, fronts);
-    else if (mmax <= 256) hipLaunchKernelGGL((k_big_panel_reg<1, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
-    else if (mmax <= 512) hipLaunchKernelGGL((k_big_panel_reg<2, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
-    else if (mmax <= 1024) hipLaunchKernelGGL((k_big_panel_reg<4, 16, 256>), dim3(count), dim3(256), 0, s, A, fronts);
-    else if (mmax <= 2048) hipLaunchKernelGGL((k_big_panel_reg<4, 8, 512>), dim3(count), dim3(512), 0, s, A, fronts);
-    else hipLaunchKernelGGL((k_big_panel_reg<8, 8, 512, false>), dim3(count), dim3(512), 0, s, A, fronts);
-    const int nt = (mmax + 63) / 64;
-    hipLaunchKernelGGL(k_big_update, dim3(nt * (nt + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
+    const int rb = (mmax + 63) / 64;
+    hipLaunchKernelGGL(k_app_diag, dim3(count), dim3(64), 0, s, A, fronts);
+    hipLaunchKernelGGL(k_app_rows, dim3(rb, count), dim3(256), 0, s, A, fronts);
+    hipLaunchKernelGGL(k_app_update, dim3(rb * (rb + 1) / 2 + rb, count), dim3(kThreads), 0, s, A, fronts, rb * (rb + 1) / 2);
+    hipLaunchKernelGGL(k_app_exact, dim3(count), dim3(512), 0, s, A, fronts);
+    hipLaunchKernelGGL(k_big_update, dim3(rb * (rb + 1) / 2, count), dim3(kThreads), 0, s, A, fronts);
     return hipGetLastError();
 }
 
@@ -4430,21 +3954,11 @@ hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int cou
     return hipGetLastError();
 }
 
-int big_panel_width(int mmax, bool app) {
-    if (app) return kAppNB;
-    static const bool legacy = getenv("UNO_KKT_BIG_LEFT") != nullptr;
-    return (legacy || mmax > 16 * kThreads) ? kBigNB : (mmax > 1024 ? 8 : 16);
-}
+int big_panel_width() { return kAppNB; }
 
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s) {
     if (A.df_nf <= 0) return hipSuccess;
-    static const size_t pad = getenv("UNO_KKT_LDS_PAD") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD")) : 0;  // diagnostics
-    if (A.mf && mmax <= 64) hipLaunchKernelGGL(k_factor_df_mf<4>, dim3(A.df_nf), dim3(64), factor_lds_bytes_mf(mmax) + pad, s, A);
-    else {
-        static const size_t lpad = getenv("UNO_KKT_LDS_PAD_LDS") ? (size_t)atol(getenv("UNO_KKT_LDS_PAD_LDS")) : 0;  // diagnostics
-        if (A.wpe2) hipLaunchKernelGGL((k_factor_df<8, 2>), dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax) + lpad, s, A);
-        else hipLaunchKernelGGL((k_factor_df<8>), dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax) + lpad, s, A);
-    }
+    hipLaunchKernelGGL((k_factor_df<8>), dim3(A.df_nf), dim3(64), factor_lds_bytes(mmax), s, A);
     return hipGetLastError();
 }
 
@@ -4459,7 +3973,6 @@ int solve_df_grid(int lds_doubles, int nf) {
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb_blk, k_solve_bwd_df, 64, sh) != hipSuccess) return 0;
     // one block per CU below the reported residency (the query can over-report by one)
     int per_cu = std::min(nf_blk, nb_blk) - 1;
-    if (getenv("UNO_KKT_DF_DEBUG")) fprintf(stderr, "[uno_kkt] df occupancy fwd %d bwd %d per CU, %d CUs, lds %zu B\n", nf_blk, nb_blk, cus, sh);
     if (per_cu < 1) return 0;
     const int64_t g = (int64_t)per_cu * cus;
     return (int)std::min<int64_t>(g, std::max(nf, 1));
@@ -4470,6 +3983,33 @@ hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int ld
     const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;
     if (forward) hipLaunchKernelGGL(k_solve_fwd_df, dim3(grid), dim3(64), sh, s, A, D);
     else hipLaunchKernelGGL(k_solve_bwd_df, dim3(grid), dim3(64), sh, s, A, D);
+    return hipGetLastError();
+}
+
+// register-resident dataflow solve kernels (k_solve_{fwd,bwd}_rg): grid = resident blocks (one below the
+// occupancy query's answer per CU, which can over-report by one), at most the walk length
+static constexpr size_t kRgFwdLds = 128 * sizeof(double) + 128 * sizeof(int32_t);
+static constexpr size_t kRgBwdLds = 8 * kRgLd * sizeof(double);
+int solve_rg_grid(bool forward, int nf) {
+    static int per_cu[2] = {-1, -1}, cus = 0;
+    const int d = forward ? 0 : 1;
+    if (per_cu[d] < 0) {
+        int dev = 0, n = 0;
+        if (hipGetDevice(&dev) != hipSuccess) return 0;
+        if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+        hipError_t e = forward ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_fwd_rg, 64, kRgFwdLds)
+                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_bwd_rg, 64, kRgBwdLds);
+        if (e != hipSuccess) return 0;
+        per_cu[d] = n - 1;
+    }
+    if (per_cu[d] < 1) return 0;
+    return (int)std::min<int64_t>((int64_t)per_cu[d] * cus, std::max(nf, 1));
+}
+
+hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, hipStream_t s) {
+    if (D.nf <= 0 || grid <= 0) return hipSuccess;
+    if (forward) hipLaunchKernelGGL(k_solve_fwd_rg, dim3(grid), dim3(64), kRgFwdLds, s, A, D);
+    else hipLaunchKernelGGL(k_solve_bwd_rg, dim3(grid), dim3(64), kRgBwdLds, s, A, D);
     return hipGetLastError();
 }
 

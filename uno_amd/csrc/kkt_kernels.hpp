@@ -70,9 +70,6 @@ struct FactorArgs {
     int stamp_mode;  // 1: phases + cycle counts, 2: write-out sub-phases in slots 4..7  // diagnostics (nullptr in normal runs): per front 8 words
     double u;
     double null_fac;
-    int mf;                     // 1: one-wave fronts on the matrix-core tile kernels (k_factor_mf / k_factor_df_mf)
-    int diag_nopiv;             // diagnostics (env UNO_KKT_DIAG_NOPIV): fronts factored with p = 0 (timing only)
-    int wpe2;                   // the m <= 64 register kernels built for 2 waves per SIMD (256 VGPRs) instead of 3
     // dataflow schedule of the upper tree (k_factor_df), after the level launches of the lower levels
     const int32_t* df_order;    // fronts, children before parents
     int32_t df_nf;
@@ -82,7 +79,6 @@ struct FactorArgs {
     uint32_t* df_ticket;        // block start order (cumulative: (epoch - 1) * df_nf at launch)
     uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
     BigFrontState* big;         // per front: state of the blocked large-front factorization (m > kMaxLdsFront)
-    int big_app;                // 1: a-posteriori kAppNB-column steps with one rank-kAppNB MFMA update (k_app_*)
 };
 
 struct SolveArgs {
@@ -182,7 +178,6 @@ struct SweepArgs {
     double* part_long;          // nf * n_long
     int max_m;
     int coalesced = 1;          // slot loads lane-contiguous (see k_sweep_front)
-    int diag_noatomic = 0;      // diagnostics only
     double* fscale = nullptr;   // per front row (layout of rows): scale[rows[t]], refreshed after every sweep
     int64_t rows_total = 0;     // front rows (length of rows / fscale / flong)
     const int8_t* flong = nullptr;  // per front row: longpos of its row (-1: not a long row); nullptr: no long rows
@@ -235,7 +230,6 @@ hipError_t launch_scatter64(const double* src, const int64_t* idx, double* dst, 
 hipError_t launch_neg(const double* b, double* r, int64_t n, hipStream_t s);  // r = -b
 hipError_t launch_sub(double* x, const double* d, int64_t n, hipStream_t s);   // x -= d
 size_t factor_lds_bytes(int mmax);
-size_t factor_lds_bytes_mf(int mmax);
 hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, int mmax, bool global, hipStream_t s);
 // one-wave solves (p <= 64, m <= kMaxLdsFront); lds_doubles >= max over the fronts of
 // p*m - p*(p-1)/2 (rounded up to even) + m (rounded up to even) + m / 2 (int32 row positions)
@@ -261,13 +255,16 @@ hipError_t launch_big_assemble(const FactorArgs& A, const int32_t* fronts, int c
 hipError_t launch_big_step(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
 hipError_t launch_big_pending(const FactorArgs& A, const int32_t* fronts, int count, int32_t* out, hipStream_t s);
 hipError_t launch_big_finish(const FactorArgs& A, const int32_t* fronts, int count, int mmax, hipStream_t s);
-int big_panel_width(int mmax, bool app);  // pivots per panel step of the large-front launches
+int big_panel_width();  // pivots per panel step of the large-front launches
 
 // dataflow factorization of the upper tree (one-wave fronts, m <= 64)
 hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
 // dataflow solve: one resident grid of one-wave blocks per direction (grid from the occupancy query)
 int solve_df_grid(int lds_doubles, int nf);
 int solve_slack_doubles();
+// register-resident dataflow solve (same DfArgs walk and hand-offs as launch_solve_df; p <= 64, m <= 128)
+int solve_rg_grid(bool forward, int nf);
+hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, hipStream_t s);
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
 // rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch.  Distributed
 // runs: the walk is the rank's own fronts, and the top rows (top_orig, eliminated on rank 0) get the
