@@ -1,6 +1,7 @@
 // HIPLDLSolver.cpp -- see HIPLDLSolver.hpp.  Each method names the MUMPS call it replaces.
 #include "HIPLDLSolver.hpp"
 
+#include <chrono>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
@@ -13,6 +14,9 @@
 
 namespace uno {
    namespace {
+      double seconds_since(std::chrono::steady_clock::time_point t0) {
+         return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      }
       void* hip_create() {
          uno_kkt_t h = nullptr;
          if (uno_kkt_create(&h, 0) != UNO_KKT_OK) return nullptr;
@@ -106,6 +110,7 @@ namespace uno {
          throw std::runtime_error("HIPLDL: the pattern changed since the symbolic analysis");
       }
       // inertia-correction retry: only the regularization diagonal (positions [0, reg_size)) changed
+      const auto t0 = std::chrono::steady_clock::now();
       const bool retry = this->in_regularization && !this->values_fresh && this->backend.factorize_update != nullptr &&
          matrix.data_pointer() == this->augmented_matrix.data_pointer();
       if (retry) {
@@ -117,6 +122,7 @@ namespace uno {
       }
       this->values_fresh = false;
       this->check(this->backend.inertia(this->handle, &this->positive, &this->negative, &this->zero), "inertia");
+      kkt_trace::profile().factorize += seconds_since(t0);
       kkt_trace::record_factorization(this->dimension, this->positive, this->negative, this->zero);
       const size_t index = kkt_trace::factor_count()++;
       if (kkt_trace::factor_hook() != nullptr) {
@@ -128,7 +134,9 @@ namespace uno {
    // MUMPSSolver.cpp:91-96 (JOB=3): the matrix argument is ignored, the last factorization is used
    void HIPLDLSolver::solve_indefinite_system(const SymmetricMatrix<size_t, double>& /*matrix*/, const Vector<double>& rhs,
          Vector<double>& result) {
+      const auto t0 = std::chrono::steady_clock::now();
       this->check(this->backend.solve(this->handle, rhs.data(), result.data()), "solve");
+      kkt_trace::profile().solve += seconds_since(t0);
       kkt_trace::record_solve(this->dimension);
    }
 
@@ -136,6 +144,9 @@ namespace uno {
    // primal-dual direction -- the orchestration every Uno plugin repeats
    void HIPLDLSolver::solve_indefinite_system(Statistics& statistics, const Subproblem& subproblem, Direction& direction,
          const WarmstartInformation& warmstart_information) {
+      auto& prof = kkt_trace::profile();
+      prof.calls++;
+      auto t0 = std::chrono::steady_clock::now();
       if (warmstart_information.objective_changed) {
          subproblem.evaluate_objective_gradient(this->objective_gradient);
       }
@@ -143,20 +154,29 @@ namespace uno {
          subproblem.evaluate_constraints(this->constraints);
          subproblem.evaluate_jacobian(this->constraint_jacobian);
       }
+      prof.evaluate += seconds_since(t0);
       if (warmstart_information.objective_changed || warmstart_information.constraints_changed) {
+         t0 = std::chrono::steady_clock::now();
          this->augmented_matrix.reset();
          subproblem.assemble_augmented_matrix(statistics, this->augmented_matrix, this->constraint_jacobian);
+         prof.assemble += seconds_since(t0);
          this->values_fresh = true;
          struct Scope {  // also reset when the loop throws (UnstableRegularization, FeasibilityRestoration.cpp:103-105)
             bool& flag;
             explicit Scope(bool& f): flag(f) { flag = true; }
             ~Scope() { flag = false; }
          } scope(this->in_regularization);
+         t0 = std::chrono::steady_clock::now();
          subproblem.regularize_augmented_matrix(statistics, this->augmented_matrix, subproblem.dual_regularization_factor(), *this);
+         prof.regularize += seconds_since(t0);
+         t0 = std::chrono::steady_clock::now();
          subproblem.assemble_augmented_rhs(this->objective_gradient, this->constraints, this->constraint_jacobian, this->rhs);
+         prof.rhs += seconds_since(t0);
       }
       this->solve_indefinite_system(this->augmented_matrix, this->rhs, this->solution);
+      t0 = std::chrono::steady_clock::now();
       subproblem.assemble_primal_dual_direction(this->solution, direction);
+      prof.direction += seconds_since(t0);
    }
 
    // MUMPSSolver.cpp:124-147 (INFOG(12), INFOG(28))

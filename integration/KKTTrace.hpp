@@ -3,6 +3,7 @@
 #ifndef UNO_KKT_TRACE_H
 #define UNO_KKT_TRACE_H
 
+#include <chrono>
 #include <cstddef>
 #include <cstdint>
 #include <vector>
@@ -31,6 +32,24 @@ namespace kkt_trace {
       return c;
    }
    inline void record_solve(size_t n) { events().push_back({'S', n, 0, 0, 0}); }
+
+   // host-time profile of the plugin's orchestration (HIPLDLSolver::solve_indefinite_system, the
+   // MUMPSSolver.cpp:98-122 sequence), seconds accumulated over the run; the driver reports it with the
+   // run's wall time, so the remainder is the Uno core's own work outside the linear-solver plugin
+   struct Profile {
+      double evaluate{0.0};     // objective gradient, constraints, Jacobian (Subproblem::evaluate_*)
+      double assemble{0.0};     // Subproblem::assemble_augmented_matrix (COO inserts into the plugin's matrix)
+      double regularize{0.0};   // Subproblem::regularize_augmented_matrix: inertia-correction loop, factorizations
+      double factorize{0.0};    //   of which: the plugin's factorize + inertia calls (device work + value upload)
+      double rhs{0.0};          // Subproblem::assemble_augmented_rhs
+      double solve{0.0};        // the plugin's solves (JOB=3)
+      double direction{0.0};    // Subproblem::assemble_primal_dual_direction
+      size_t calls{0};
+   };
+   inline Profile& profile() {
+      static Profile p;
+      return p;
+   }
 } // namespace kkt_trace
 
 #endif

@@ -7,6 +7,7 @@
 // usage: uno_kkt_driver <model> [option=value ...]     model: hs015 (hand-coded), arrowband:<N> (synthetic NLP) or a path to a text .nl file
 //        uno_kkt_driver convexify:<model> [option=value ...]   byrd-preset Hessian convexification only (see below)
 #include <cmath>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
@@ -260,7 +261,9 @@ int main(int argc, char* argv[]) {
 
       Uno uno{model->number_constraints, options};
       NoUserCallbacks callbacks{};
+      const auto t_solve = std::chrono::steady_clock::now();
       const Result result = uno.solve(*model, initial_iterate, options, callbacks);
+      const double wall = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_solve).count();
 
       std::printf("{\"model\": \"%s\", \"linear_solver\": \"%s\", \"status\": %d, \"iterations\": %zu, \"objective\": %.17g",
          model_name.c_str(), options.get_string("linear_solver").c_str(), static_cast<int>(result.optimization_status),
@@ -305,7 +308,15 @@ int main(int argc, char* argv[]) {
             static_cast<long long>(e.negative), static_cast<long long>(e.zero));
          first = false;
       }
-      std::printf("], \"crosscheck\": [");
+      {
+         const auto& pr = kkt_trace::profile();
+         const double plugin = pr.evaluate + pr.assemble + pr.regularize + pr.rhs + pr.solve + pr.direction;
+         std::printf("], \"host_profile_s\": {\"wall\": %.6f, \"plugin_orchestration\": %.6f, \"evaluate\": %.6f, "
+            "\"assemble_coo\": %.6f, \"regularize\": %.6f, \"factorize_inertia\": %.6f, \"rhs\": %.6f, \"solve\": %.6f, "
+            "\"direction\": %.6f, \"uno_core_outside_plugin\": %.6f, \"orchestration_calls\": %zu}", wall, plugin, pr.evaluate,
+            pr.assemble, pr.regularize, pr.factorize, pr.rhs, pr.solve, pr.direction, wall - plugin, pr.calls);
+      }
+      std::printf(", \"crosscheck\": [");
       for (size_t k = 0; k < crosscheck_records.size(); ++k) std::printf("%s%s", k ? ", " : "", crosscheck_records[k].c_str());
       std::printf("]}\n");
    }

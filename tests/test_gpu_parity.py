@@ -212,7 +212,7 @@ def test_dataflow_solve_kernels_bit_identical(uno_amd, rg):
     epochs) and after a refactorization with new values."""
     from uno_amd import arrowband, SEEDS, HipKKT
     n, nv, m, r, c, v, b = arrowband(100000, SEEDS["C3"])
-    gd, gl = HipKKT(0, solve_rg=rg), HipKKT(0, dataflow_solve=0)
+    gd, gl = HipKKT(0, solve_rg=rg), HipKKT(0, dataflow_solve=0, solve_rg=rg)
     for g in (gd, gl):
         g.analyze(n, r, c)
         g.factorize(v)

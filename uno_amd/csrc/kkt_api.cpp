@@ -190,6 +190,9 @@ struct uno_kkt {
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
     int solve_rg = 1;              // option "solve_rg": register-resident dataflow kernels (k_solve_*_rg)
     int rg_grid_f = 0, rg_grid_b = 0;
+    bool rg_fwd_ok = false;        // the walk meets k_solve_fwd_rg's precondition (every front p <= 32, m <= 72)
+    bool new_bwd = false;          // option solve_rg: the backward of one-wave fronts runs the register kernels' arithmetic
+                                   // in both schedules (k_solve_bwd_rg / k_solve_bwd_w2)
     int df_win = 0, df_win_opt = 0; // LDS panel window of the dataflow solve (option solve_window, 0 = auto)
     int df_piv_off = 0;
     uint32_t df_epoch = 0;
@@ -198,6 +201,8 @@ struct uno_kkt {
     int df_consec_aborts = 0;      // consecutive aborted dataflow solves (kMaxDfAborts turns the walk off)
     int debug_abort_solves = 0;    // option debug_abort_solves: the next k dataflow solves start with the abort flag set (tests)
     DBuf<int32_t> df_order, df_desc, df_xpos, df_rxpos;
+    DBuf<int32_t> rg_desc, ov_desc;  // register kernels: the walk split into p <= 32, m <= 72 fronts and the others
+    int32_t rg_nf = 0, ov_nf = 0, ov_grid = 0;
     DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
     DBuf<uint32_t> df_cnt, df_done, df_abort;
     DBuf<double> df_cvx, df_xs;
@@ -369,6 +374,8 @@ DfArgs dataflow_args(uno_kkt_t h) {
     D.win = h->df_win;
     D.piv_off = h->df_piv_off;
     D.stamps = h->want_solve_stamps ? h->df_stamps.p : nullptr;
+    D.rg_desc = h->rg_desc.p; D.rg_nf = h->rg_nf;
+    D.ov_desc = h->ov_desc.p; D.ov_nf = h->ov_nf; D.ov_grid = h->ov_grid;
     return D;
 }
 
@@ -900,8 +907,20 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
     return hipSuccess;
 }
 
+// the register kernels' launch: resident blocks (occupancy), the last ov_grid of them walk the oversized fronts
+void set_rg_grids(uno_kkt_t h) {
+    h->ov_grid = std::min(h->ov_nf, 32);
+    for (int d = 0; d < 2; ++d) {
+        const int resident = solve_rg_grid(d == 0, 1 << 30);
+        int g = std::min(resident, h->rg_nf + h->ov_grid);
+        if (resident <= h->ov_grid || (h->rg_nf > 0 && g - h->ov_grid < 1)) g = 0;  // no room: df kernels
+        (d == 0 ? h->rg_grid_f : h->rg_grid_b) = g;
+    }
+}
+
 hipError_t setup_dataflow(uno_kkt_t h) {
     const Symbolic& S = h->S;
+    h->new_bwd = h->solve_rg != 0;
     h->df_grid = 0;
     h->df_rx_valid = false;
     h->df_epoch = 0;
@@ -914,7 +933,7 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     for (int32_t f : S.level_fronts)
         if (!dist || h->dist.part.owner[f] == h->rank) walk.push_back(f);
     if (walk.empty()) return hipSuccess;
-    int max_sz = 0, mmax = 0;
+    int max_sz = 0, mmax = 0, pmax = 0;
     for (int32_t f : walk) {
         const int m = S.f_m[f], p = S.f_p[f];
         if (p > 64 || m > kMaxLdsFront) {  // a front needs the 256-thread kernels
@@ -923,7 +942,9 @@ hipError_t setup_dataflow(uno_kkt_t h) {
         }
         max_sz = std::max(max_sz, p * m - p * (p - 1) / 2);
         mmax = std::max(mmax, m);
+        pmax = std::max(pmax, p);
     }
+    h->rg_fwd_ok = true;  // fronts beyond the register class take the kernels' LDS-panel path
     // panel window: sized so that 16 one-wave blocks (4 per SIMD, the register limit of the dataflow
     // kernels) fit the 160 KB LDS of a CU; larger panels are processed in column windows
     const int rows_lds = ((mmax + 1) & ~1) + (mmax + 1) / 2;
@@ -973,6 +994,19 @@ hipError_t setup_dataflow(uno_kkt_t h) {
             put64(d + kDescCvx, cvx[f]); put64(d + kDescXs, xs[f]);
         }
         if ((e = h->df_desc.upload(desc, s)) != hipSuccess) return e;
+        // the register kernels' two walks (same order): p <= 32, m <= 72 fronts, and the rest
+        std::vector<int32_t> rgd, ovd;
+        for (size_t t = 0; t < walk.size(); ++t) {
+            const int32_t f = walk[t];
+            auto& dst = (S.f_p[f] <= 32 && S.f_m[f] <= 72) ? rgd : ovd;
+            dst.insert(dst.end(), desc.begin() + 16 * t, desc.begin() + 16 * (t + 1));
+        }
+        h->rg_nf = (int32_t)(rgd.size() / 16);
+        h->ov_nf = (int32_t)(ovd.size() / 16);
+        if (rgd.empty()) rgd.assign(16, 0);
+        if (ovd.empty()) ovd.assign(16, 0);
+        if ((e = h->rg_desc.upload(rgd, s)) != hipSuccess) return e;
+        if ((e = h->ov_desc.upload(ovd, s)) != hipSuccess) return e;
     }
     if ((e = h->df_cvx_off.upload(cvx, s)) != hipSuccess) return e;
     if ((e = h->df_ch_cvx_off.upload(chx, s)) != hipSuccess) return e;
@@ -990,8 +1024,7 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     h->df_lds = lds;
     h->df_nwalk = (int32_t)walk.size();
     h->df_grid = solve_df_grid(lds, h->df_nwalk);
-    h->rg_grid_f = solve_rg_grid(true, h->df_nwalk);
-    h->rg_grid_b = solve_rg_grid(false, h->df_nwalk);
+    set_rg_grids(h);
     if (h->verbose)
         fprintf(stderr, "[uno_kkt] dataflow solve: %d of %lld fronts, panel window %d of %d doubles, lds %d doubles, grid %d\n",
                 h->df_nwalk, (long long)S.nf, win, max_sz, lds, h->df_grid);
@@ -1521,7 +1554,17 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }
-    else if (n == "solve_rg") h->solve_rg = value != 0.0;
+    else if (n == "solve_rg") {
+        h->solve_rg = value != 0.0;
+        if (h->analyzed) {
+            HIPCHK(h, setup_dataflow(h));
+            HIPCHK(h, hipStreamSynchronize(h->stream));
+        }
+    }
+    else if (n == "solve_rg_wpe") {
+        set_solve_rg_wpe((int)value);
+        if (h->analyzed) set_rg_grids(h);
+    }
     else if (n == "dataflow_solve") {
         h->df_enabled = value != 0.0;
         if (h->analyzed) {
@@ -1742,6 +1785,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
     A.ch_relmap_off = h->ch_relmap_off.p;
     auto run = [&](const Plan& P, const SolveLaunch& L, bool forward) -> hipError_t {
         const int32_t* fr = P.sol_fronts.p + L.begin;
+        if (L.wave && !forward && h->new_bwd) return launch_solve_bwd_w2(A, fr, L.count, s);
         return L.wave ? launch_solve_wave(A, fr, L.count, L.lds, forward, s)
                       : launch_solve(A, fr, L.count, L.mmax, L.pmax, forward, s);
     };
@@ -1754,7 +1798,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
     DfArgs Df;
     auto walk = [&](bool forward) -> hipError_t {
         const int g = forward ? h->rg_grid_f : h->rg_grid_b;
-        if (h->solve_rg && forward && g > 0) return launch_solve_rg(A, Df, g, forward, s);
+        if (h->solve_rg && h->rg_fwd_ok && (forward || h->new_bwd) && g > 0) return launch_solve_rg(A, Df, g, forward, s);
         return launch_solve_df(A, Df, h->df_grid, h->df_lds, forward, s);
     };
     if (df) {

@@ -2635,7 +2635,77 @@ __device__ __forceinline__ double ld_clamped(const double* base, int rel, int n)
 }
 
 
-struct RgFwdIn {
+// Fronts outside the register kernels' class (p > 32 or m > 72: in practice a few parents enlarged by delayed
+// columns) form a second walk (DfArgs::ov_*, the same topological order) that the last ov_grid blocks of the
+// launch process with the LDS-panel per-front code of k_solve_{fwd,bwd}_df (same arithmetic) in a window of
+// kRgWin doubles; the hand-offs are the per-front counters, so the two walks wait on each other as any two
+// blocks do.  The roles split at the top of the kernel: the register fast path keeps its own budget.
+constexpr int kRgWin = 512;                         // doubles (> one column of a front of <= 128 rows)
+constexpr int kRgRegion = kRgWin + kSolveSlack;     // the window and its read slack
+__device__ __forceinline__ bool rg_fits(int m, int p) { return p <= 32 && m <= 72; }
+
+// forward of one oversized front (over role): y (128) and fpl (128 words) at smem, window P after them
+__device__ void rg_fwd_over(const SolveArgs& A, const DfArgs& D, const FrontRec& r, double* y, int32_t* fpl, double* P) {
+    const int lane = threadIdx.x;
+    const int m = r.m, p = r.p, f = r.f;
+    const int64_t ro = r.ro;
+    const int mypiv = lane < p ? (int)A.piv[ro + lane] : 0;
+    const double e0 = lane < p ? D.xs[r.woff + lane] : 0.0;
+    int my_cm = 0;
+    long long my_rmo = 0, my_cxo = 0;
+    if (lane < r.c1 - r.c0) {
+        my_cm = A.ch_cm[r.c0 + lane];
+        my_rmo = A.ch_relmap_off[r.c0 + lane];
+        my_cxo = D.ch_cvx_off[r.c0 + lane];
+    }
+    y[lane] = e0;
+    y[lane + 64] = 0.0;
+    fpl[lane] = lane < m ? A.fpos[ro + lane] : 0;
+    fpl[lane + 64] = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
+    if (r.c1 > r.c0) {
+        df_wait(D.cnt + f, D.epoch * (uint32_t)(r.c1 - r.c0), D.abort_flag);
+        __syncthreads();
+        fwd_extend_add<true>(A, D, r.c0, r.c1, my_cm, my_rmo, my_cxo, y, fpl);
+    }
+    __syncthreads();
+    const int k1 = fwd_chunk_end(m, p, 0, kRgWin);
+    stage_panel<4>(A.L, r.Lo, cstart(m, k1), P);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    fwd_compute_win2(A.L, r.Lo, m, p, P, kRgWin, k1, y, mypiv, D.xs + r.woff + lane, D.cvx + r.xoff);
+    drain_stores();
+    if (r.par >= 0 && lane == 0) __hip_atomic_fetch_add(D.cnt + r.par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // LDS reused by the next front
+}
+
+// the backward arithmetic of an oversized front (bwd_compute_win2 from the last window), x in X (LDS)
+__device__ __forceinline__ double rg_bwd_over_core(const double* __restrict__ L, int64_t Lo, int m, int p, double* P,
+                                                   const double* X, int mypiv) {
+    const int c0 = bwd_chunk_begin(m, p, p, kRgWin);
+    const int base = cstart(m, c0);
+    stage_panel<4>(L, Lo + base, cstart(m, p) - base, P);
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    return bwd_compute_win2(L, Lo, m, p, P, kRgWin, c0, X, mypiv);
+}
+
+// backward of one oversized front (over role): X (128 doubles: the rows' values) at smem, window P after it
+__device__ void rg_bwd_over(const SolveArgs& A, const DfArgs& D, const FrontRec& r, double* X, double* P) {
+    const int lane = threadIdx.x;
+    const int m = r.m, p = r.p;
+    const int64_t ro = r.ro;
+    const int mypiv = lane < p ? (int)A.piv[ro + lane] : (int)PIV_NULL;
+    if (r.par >= 0) df_wait(D.done + r.par, D.epoch, D.abort_flag);
+    for (int i = lane; i < m; i += 64) X[i] = i < p ? D.xs[r.woff + i] : ld_sc1(D.xs + D.rxpos[ro + i]);
+    const double xj = rg_bwd_over_core(A.L, r.Lo, m, p, P, X, mypiv);
+    if (lane < p) st_sc1(D.xs + r.woff + lane, xj);
+    drain_stores();
+    if (lane == 0) __hip_atomic_store(D.done + r.f, D.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // LDS reused by the next front
+}
+
+// per-front loads of the forward walk other than the panel columns
+struct RgFwdMeta {
     int piv;                    // lane < p: pivot kind
     double e0;                  // lane < p: right-hand side at the own pivots (xs)
     int32_t fp0, fp1;           // pivoted positions of the analysis-order rows lane, lane + 64
@@ -2643,11 +2713,11 @@ struct RgFwdIn {
     long long my_rmo, my_cxo;   // children's edge records (lane < children)
     uint32_t dep;               // arrival counter as seen at issue time (sc1)
     double dgl, sbl;            // L(lane, lane), L(lane, lane - 1): the diagonal blocks of D
-    double B[kRgCols];          // B[u] = L(lane, k0 + u)
+    double H[4];                // rows 64..71: H[c] = L(64 + (lane & 7), 8c + (lane >> 3))
 };
 
-// L(row0 + lane, k0 + u) -> B[u], u < kRgCols (indices clamped into the front's panel: lanes / columns
-// outside it read a harmless in-panel value that no step uses)
+// L(row0 + lane, k0 + u) -> B[u] for the front's columns k0 + u < p (uniform guards: only those are loaded;
+// row indices clamped into the panel: rows outside it read a harmless in-panel value that no step uses)
 __device__ __forceinline__ void rg_load_cols(const double* __restrict__ L, int64_t Lo, int m, int p, int k0, int row0,
                                              double (&B)[kRgCols]) {
     const int lane = threadIdx.x;
@@ -2656,13 +2726,24 @@ __device__ __forceinline__ void rg_load_cols(const double* __restrict__ L, int64
 #pragma unroll
     for (int u = 0; u < kRgCols; ++u) {
         const int k = k0 + u;
-        const int rel = cs + row0 + lane - k;
-        if (k < p) B[u] = ld_clamped(L + Lo, rel, sz);  // uniform: only the front's columns are loaded
+        if (k < p) B[u] = ld_clamped(L + Lo, cs + row0 + lane - k, sz);
         cs += m - k;
     }
 }
 
-__device__ __forceinline__ void rg_fwd_issue(const SolveArgs& A, const DfArgs& D, const FrontRec& r, RgFwdIn& q) {
+// rows 64..71 of the panel (m <= 72, p <= 32), compact: H[c] = L(64 + (lane & 7), 8c + (lane >> 3))
+__device__ __forceinline__ void rg_load_high(const double* __restrict__ L, int64_t Lo, int m, int p, double (&H)[4]) {
+    const int lane = threadIdx.x;
+    const int sz = p * m - ((p * (p - 1)) >> 1);
+    const int rr = lane & 7, kk = lane >> 3;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+        const int col = 8 * c + kk;
+        if (8 * c < p) H[c] = ld_clamped(L + Lo, cstart(m, col) + 64 + rr - col, sz);
+    }
+}
+
+__device__ __forceinline__ void rg_fwd_meta(const SolveArgs& A, const DfArgs& D, const FrontRec& r, RgFwdMeta& q) {
     const int lane = threadIdx.x;
     const int m = r.m, p = r.p;
     const int64_t ro = r.ro;
@@ -2681,7 +2762,7 @@ __device__ __forceinline__ void rg_fwd_issue(const SolveArgs& A, const DfArgs& D
     const int lc = lane < p ? lane : 0;
     q.dgl = A.L[r.Lo + cstart(m, lc)];
     q.sbl = lane > 0 && lane < p ? A.L[r.Lo + cstart(m, lane - 1) + 1] : 0.0;
-    rg_load_cols(A.L, r.Lo, m, p, 0, 0, q.B);
+    if (m > 64) rg_load_high(A.L, r.Lo, m, p, q.H);  // uniform (walk precondition: m <= 72, p <= 32)
 }
 
 // children's update vectors -> y (LDS rows, permuted by fpl), two children's loads in flight at a time
@@ -2725,24 +2806,51 @@ __device__ __forceinline__ void rg_extend_add(const SolveArgs& A, const DfArgs& 
     }
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_fwd_rg(SolveArgs A, DfArgs D) {
+// The walk issues the next front's loads under the current front's work: its metadata right after the
+// current front's children are assembled, and its panel column u into register B[u] as soon as step u of
+// the current front has consumed B[u] (rolling prefetch).  Walk precondition (setup_dataflow): every front
+// has p <= 32 and m <= 72 (rows 64..71 go through a small LDS tile, Th); other walks use k_solve_fwd_df.
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_solve_fwd_rg(SolveArgs A, DfArgs D) {
     extern __shared__ __attribute__((aligned(16))) double smem_s[];
     const int lane = threadIdx.x;
-    const int G = gridDim.x;
+    double* y = smem_s;                          // 128 doubles: the front's rows (pivoted order)
+    int32_t* fpl = (int32_t*)(smem_s + 128);     // 128 words
+    const int G = (int)gridDim.x - D.ov_grid;
+    if ((int)blockIdx.x >= G) {  // over role: the oversized fronts' walk
+        for (int t = blockIdx.x - G; t < D.ov_nf; t += D.ov_grid) {
+            const FrontRec r = df_record(D.ov_desc[t * 16 + (lane & 15)]);
+            unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)r.f : nullptr;
+            if (st && lane == 0) st[0] = st[1] = __builtin_amdgcn_s_memrealtime();
+            rg_fwd_over(A, D, r, y, fpl, smem_s + 192);
+            if (st && lane == 0) st[2] = st[3] = __builtin_amdgcn_s_memrealtime();
+        }
+        return;
+    }
     int t = blockIdx.x;
-    if (t >= D.nf) return;
-    double* y = smem_s;                         // 128 doubles: the front's rows (pivoted order)
-    int32_t* fpl = (int32_t*)(smem_s + 128);    // 128 words
-    FrontRec r = df_record(df_desc_load(D, t));
-    RgFwdIn q;
-    rg_fwd_issue(A, D, r, q);
-    int dn = df_desc_load(D, min(t + G, D.nf - 1));
+    if (t >= D.rg_nf) return;
+    double* Th = smem_s + 192;                   // 8 x 33 doubles: rows 64..71 of the panel
+    const int* desc = D.rg_desc;
+    FrontRec r = df_record(desc[t * 16 + (lane & 15)]);
+    RgFwdMeta q;
+    double B[kRgCols];
+    rg_fwd_meta(A, D, r, q);
+    rg_load_cols(A.L, r.Lo, r.m, r.p, 0, 0, B);
+    int dn = desc[min(t + G, D.rg_nf - 1) * 16 + (lane & 15)];
     for (;;) {
         const int m = r.m, p = r.p, f = r.f, par = r.par;
+        const int64_t xoff = r.xoff, woff = r.woff;
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f : nullptr;
         if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
         const unsigned long long liveM = __ballot(lane < p && q.piv != PIV_NULL);
         const unsigned long long twoAM = __ballot(lane < p && q.piv == PIV_2X2_A);
+        const int piv_c = q.piv;
+        const double dgl = q.dgl, sbl = q.sbl;
+        if (m > 64) {  // uniform
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (8 * c < p) Th[(lane & 7) * 33 + 8 * c + (lane >> 3)] = q.H[c];
+        }
         y[lane] = q.e0;
         y[lane + 64] = 0.0;
         fpl[lane] = q.fp0;
@@ -2755,43 +2863,56 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         double y0 = y[lane];
         double a1 = m > 64 ? y[lane + 64] : 0.0;
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-        // pivot steps on the rows < 64, columns in register rounds of kRgCols
-        for (int k0 = 0; k0 < p; k0 += kRgCols) {
-            if (k0 > 0) rg_load_cols(A.L, r.Lo, m, p, k0, 0, q.B);
+        const int tn = t + G;
+        const bool more = tn < D.rg_nf;
+        FrontRec rn = r;
+        asm volatile("" ::: "memory");  // the next front's loads stay below this front's assembly
+        if (more) {
+            rn = df_record(dn);
+            dn = desc[min(tn + G, D.rg_nf - 1) * 16 + (lane & 15)];
+            rg_fwd_meta(A, D, rn, q);
+        } else {
+            rn.p = 0;
+        }
+        // the pivot steps on the rows < 64; the next front's column u goes into B[u] once step u has used it
+        {
+            const int sz_n = rn.p * rn.m - ((rn.p * (rn.p - 1)) >> 1);
+            int cs_n = 0;  // cstart(rn.m, u)
 #pragma unroll
             for (int u = 0; u < kRgCols; ++u) {
-                const int k = k0 + u;
-                if (k < p) {  // uniform
-                    const double yb = readlane_d(y0, k);
-                    const double yk = (liveM >> k) & 1 ? yb : 0.0;
-                    const int lim = (twoAM >> k) & 1 ? k + 1 : k;
-                    const double tv = y0 - q.B[u] * yk;
+                if (u < p) {  // uniform
+                    const double yb = readlane_d(y0, u);
+                    const double yk = (liveM >> u) & 1 ? yb : 0.0;
+                    const int lim = (twoAM >> u) & 1 ? u + 1 : u;
+                    const double tv = y0 - B[u] * yk;
                     y0 = lane > lim ? tv : y0;
                 }
+                if (u < rn.p) {  // uniform
+                    B[u] = ld_clamped(A.L + rn.Lo, cs_n + lane - u, sz_n);
+                    cs_n += rn.m - u;
+                }
+                __builtin_amdgcn_sched_barrier(0);  // keep the load behind the step that frees its register
             }
         }
-        // rows 64..m-1: the same column updates with the values the steps broadcast (y_k, 0 for a null pivot)
+        // rows 64..71: the same column updates with the values the steps broadcast (y_k, 0 for a null pivot),
+        // from the LDS tile, lane = row - 64
         if (m > 64) {
             const double ybv = lane < p && ((liveM >> lane) & 1) ? y0 : 0.0;
-            for (int k0 = 0; k0 < p; k0 += kRgCols) {
-                rg_load_cols(A.L, r.Lo, m, p, k0, 64, q.B);
+            const int rw = lane < 8 ? lane : 0;
 #pragma unroll
-                for (int u = 0; u < kRgCols; ++u) {
-                    const int k = k0 + u;
-                    if (k < p) a1 -= q.B[u] * readlane_d(ybv, k);
-                }
-            }
+            for (int k = 0; k < kRgCols; ++k)
+                if (k < p) a1 -= Th[rw * 33 + k] * readlane_d(ybv, k);
         }
         // update vector (rows >= p) and the own pivots' z = D^-1 y
-        double* cvo = D.cvx + r.xoff;
+        double* cvo = D.cvx + xoff;
         if (lane >= p && lane < m) st_sc1(cvo + (lane - p), y0);
         if (lane + 64 < m) st_sc1(cvo + (lane + 64 - p), a1);
         {
-            const double dg = q.dgl, sb = q.sbl;
+            const double dg = dgl, sb = sbl;
             const double dgn = __shfl(dg, lane < 63 ? lane + 1 : lane), sbn = __shfl(sb, lane < 63 ? lane + 1 : lane);
             const double dgp = __shfl(dg, lane > 0 ? lane - 1 : 0);
             const double yn = __shfl(y0, lane < 63 ? lane + 1 : lane), yp = __shfl(y0, lane > 0 ? lane - 1 : 0);
-            const int kind = q.piv;
+            const int kind = piv_c;
             double out = 0.0;  // null pivot contributes 0
             if (kind == PIV_1X1) {
                 out = y0 / dg;
@@ -2802,179 +2923,248 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
                 const double yA = first ? y0 : yp, yB = first ? yn : y0;
                 out = first ? (e * yA - b * yB) / det : (a * yB - b * yA) / det;
             }
-            if (lane < p) D.xs[r.woff + lane] = out;
+            if (lane < p) D.xs[woff + lane] = out;
         }
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
-        // the next front's loads go out before this front's stores are drained
-        const int tn = t + G;
-        const bool more = tn < D.nf;
-        asm volatile("" ::: "memory");  // the next front's loads are not hoisted above this front's work
-        if (more) {
-            r = df_record(dn);
-            dn = df_desc_load(D, min(tn + G, D.nf - 1));
-            rg_fwd_issue(A, D, r, q);
-        }
         drain_stores();
         if (par >= 0 && lane == 0) __hip_atomic_fetch_add(D.cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (!more) break;
+        r = rn;
         t = tn;
     }
 }
 
-// backward: window geometry of a front (OCT column octets per 8-row window)
-struct RgBwdIn {
-    int piv;          // lane < p: pivot kind
-    double e0;        // lane < p: z (forward result)
-    int32_t a0, a1;   // xs index of the rows lane, lane + 64 (>= p): the ancestors' solution values
-    uint32_t dep;     // parent's done word as seen at issue time (sc1)
-    double B[kRgSlots];
-};
-
-// windows: q < nr: rectangle rows [p + 8q, ..), else triangle rows [8t, ..), t = nt - 1 - (q - nr)
-__device__ __forceinline__ int rg_win_row(int m, int p, int q) {
-    const int nr = (m - p + 7) >> 3, nt = (p + 7) >> 3;
-    return q < nr ? p + 8 * q : 8 * (nt - 1 - (q - nr));
+// ---- register-resident backward (fronts with p <= 32, m <= 72) ----
+// Lane = row, as the forward: B[j] = L(lane, j) (j < p), H the rows 64..71.  The rectangle's column sums
+// s_j = sum_{i >= p} L(i, j) x_i are one transpose-reduction across the wave: the 32 per-lane products
+// are halved by v_permlane32_swap / v_permlane16_swap exchanges (lane bits 5, 4) and shuffles (bits 3, 2,
+// 1), so lane 2c ends with column c's sum, summed in a fixed tree order; rows 64..71 add their column sums
+// (8-lane reductions) after it.  The triangle goes through an LDS tile T[i * 33 + j] = L(i, j) (stride 33:
+// conflict-free writes down a column, contiguous reads along a row) and runs lane = column, steps
+// k = p-1 .. 0 as bwd_compute.  The level-scheduled solve of such fronts (k_solve_bwd_w2) calls the same
+// core, so both schedules stay bit-identical; handles whose one-wave fronts all fit use it (new_bwd).
+__device__ __forceinline__ void dswap32(double& a, double& b) {  // a: vdst, b: vsrc of v_permlane32_swap
+    const unsigned long long ua = as_bits(a), ub = as_bits(b);
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    a = as_double(((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]);
+    b = as_double(((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]);
 }
+__device__ __forceinline__ void dswap16(double& a, double& b) {  // v_permlane16_swap: odd rows of a <-> even rows of b
+    const unsigned long long ua = as_bits(a), ub = as_bits(b);
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)ua, (unsigned)ub, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(ua >> 32), (unsigned)(ub >> 32), false, false);
+    a = as_double(((unsigned long long)(unsigned)hi[0] << 32) | (unsigned)lo[0]);
+    b = as_double(((unsigned long long)(unsigned)hi[1] << 32) | (unsigned)lo[1]);
+}
+__device__ __forceinline__ double shfl_xor_d(double v, int mask) { return bperm_d(v, (int)(threadIdx.x ^ mask)); }
 
-// Window pieces: a chunk is one window's columns [32 h, 32 h + 32) (h = 0, and h = 1 when p > 32), as four
-// 8 x 8 pieces; piece c of chunk g: lane l holds L(row0 + (l & 7), 32 h + 8 c + (l >> 3)).  One register
-// round holds kRgSlots / 4 = 8 chunks (fronts of C3: every window of the front).
-constexpr int kRgLd = 66;  // LDS row stride of a window tile (doubles, 2 mod 32)
-__device__ __forceinline__ void rg_load_windows(const double* __restrict__ L, int64_t Lo, int m, int p, int g0,
-                                                double (&B)[kRgSlots]) {
+// The backward of one front (see above).  After B has been consumed (T written, products formed and halved
+// three times), next() is called: the walk issues the next front's loads into B there.  Returns x_j in lane j < p.
+template <class Next>
+__device__ __forceinline__ double rg_bwd_core(double (&B)[kRgCols], const double (&H)[4], double xr0, double xh, int m,
+                                              int p, int piv, double* T, Next next) {
     const int lane = threadIdx.x;
-    const int rr = lane & 7, kk = lane >> 3;
-    const int sz = p * m - ((p * (p - 1)) >> 1);
-    const int hs = p > 32 ? 1 : 0;
+    constexpr int ld = 33;
+    const bool live = lane < p && piv != PIV_NULL;
+    const unsigned long long liveM = __ballot(live);
+    const unsigned long long twoBM = __ballot(lane < p && piv == PIV_2X2_B);
+    // triangle tile: row lane (< p), columns j < p
 #pragma unroll
-    for (int w = 0; w < kRgSlots / 4; ++w) {
-        const int g = g0 + w;
-        const int a = rg_win_row(m, p, g >> hs);
-        const int h = g & hs;
+    for (int j = 0; j < kRgCols; ++j)
+        if (j < p && lane < p) T[lane * ld + j] = B[j];  // j: uniform
+    // rectangle products (rows p <= lane < m), first halving: lanes < 32 keep columns 0..15, lanes >= 32 16..31.
+    // Each product's rounding error e = fma(l, x, -l x) is carried through the first two halvings in its own
+    // tree and added back there, so the products enter the sum exactly (as in bwd_compute's FMA accumulation)
+    const bool rowok = lane >= p && lane < m;
+    double r2[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {  // columns j, j + 8, j + 16, j + 24: two halvings (lane bits 5, 4)
+        double r1[2], e1[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const int c = j + 8 * h;
+            const double la = rowok && c < p ? B[c] : 0.0, lb = rowok && c + 16 < p ? B[c + 16] : 0.0;
+            double a = la * xr0, b = lb * xr0;
+            double ea = fma(la, xr0, -a), eb = fma(lb, xr0, -b);
+            dswap32(a, b);
+            dswap32(ea, eb);
+            r1[h] = a + b;
+            e1[h] = ea + eb;
+        }
+        double a = r1[0], b = r1[1], ea = e1[0], eb = e1[1];
+        dswap16(a, b);
+        dswap16(ea, eb);
+        r2[j] = (a + b) + (ea + eb);
+    }
+    const bool b3 = (lane >> 3) & 1, b2 = (lane >> 2) & 1, b1 = (lane >> 1) & 1;
+    double r3[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const double keep = b3 ? r2[j + 4] : r2[j], send = b3 ? r2[j] : r2[j + 4];
+        r3[j] = keep + shfl_xor_d(send, 8);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    next();  // B is free and the products are down to four registers per lane
+    double r4[2];
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+        const double keep = b2 ? r3[j + 2] : r3[j], send = b2 ? r3[j] : r3[j + 2];
+        r4[j] = keep + shfl_xor_d(send, 4);
+    }
+    const double keep5 = b1 ? r4[1] : r4[0], send5 = b1 ? r4[0] : r4[1];
+    const double r5 = keep5 + shfl_xor_d(send5, 2);
+    const double r6 = r5 + shfl_xor_d(r5, 1);          // lane 2c, 2c + 1: column c
+    double sj = bperm_d(r6, (2 * lane) & 63);          // lane j < 32: column j
+    if (m > 64) {  // uniform: rows 64..71, 8-lane groups of one column (lane >> 3) per H[c]
+        const int rr = lane & 7;
+        double hs[4];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
-            const int col = 32 * h + 8 * c + kk;
-            if (32 * h + 8 * c < p) B[w * 4 + c] = ld_clamped(L + Lo, cstart(m, col) + a + rr - col, sz);  // uniform
+            double v = 8 * c < p && 64 + rr < m ? H[c] * xh : 0.0;
+            v += shfl_xor_d(v, 1);
+            v += shfl_xor_d(v, 2);
+            v += shfl_xor_d(v, 4);
+            hs[c] = v;  // column 8c + (lane >> 3)
         }
+        const int src = 8 * (lane & 7);  // lane j reads column j = 8c + g from lane 8g, c = j >> 3
+        double h = 0.0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            const double v = bperm_d(hs[c], src);
+            h = (lane >> 3) == c ? v : h;
+        }
+        sj += h;
     }
-}
-
-__device__ __forceinline__ void rg_bwd_issue(const SolveArgs& A, const DfArgs& D, const FrontRec& r, RgBwdIn& q) {
-    const int lane = threadIdx.x;
-    const int m = r.m, p = r.p;
-    const int64_t ro = r.ro;
-    q.piv = lane < p ? (int)A.piv[ro + lane] : (int)PIV_NULL;
-    q.e0 = lane < p ? D.xs[r.woff + lane] : 0.0;
-    q.a0 = lane < m && lane >= p ? D.rxpos[ro + lane] : 0;
-    q.a1 = lane + 64 < m ? D.rxpos[ro + lane + 64] : 0;
-    q.dep = r.par >= 0 ? ld_sc1_u32(D.done + r.par) : 0u;
-    rg_load_windows(A.L, r.Lo, m, p, 0, q.B);
-}
-
-// the windows of one front, lane = column j: rectangle dot products (two accumulators by row parity, as
-// bwd_compute), then the triangle's rows descending; x (LDS) holds the rows' values, T one window
-__device__ __forceinline__ double rg_bwd_front(const SolveArgs& A, const FrontRec& r, RgBwdIn& q, unsigned long long liveM,
-                                               unsigned long long twoBM, double xr0, double xr1, double* T, double xj) {
-    const int lane = threadIdx.x;
-    const int m = r.m, p = r.p;
-    constexpr int ld = kRgLd;
-    constexpr int NG = kRgSlots / 4;
-    const int rr = lane & 7, kk = lane >> 3;
-    const int nr = (m - p + 7) >> 3, nt = (p + 7) >> 3;
-    const int hs = p > 32 ? 1 : 0;
-    const int nchunk = (nr + nt) << hs;
-    const bool live = lane < p && q.piv != PIV_NULL;
-    double s0 = 0.0, s1 = 0.0;
-    for (int g0 = 0; g0 < nchunk; g0 += NG) {
-        if (g0 > 0) rg_load_windows(A.L, r.Lo, m, p, g0, q.B);
+    double xj = lane < p ? xr0 : 0.0;
+    if (live) xj -= sj;
+    // triangle: steps k = p-1 .. 0, eight LDS rows read ahead
+    for (int kh = p - 1; kh >= 0; kh -= 8) {
+        double lv[8];
 #pragma unroll
-        for (int w = 0; w < NG; ++w) {
-            const int g = g0 + w;
-            if (g >= nchunk) continue;  // uniform
-            const int h = g & hs;
+        for (int u = 0; u < 8; ++u) lv[u] = T[max(kh - u, 0) * ld + lane];  // L(k, lane), lane < k
 #pragma unroll
-            for (int c = 0; c < 4; ++c)
-                if (32 * h + 8 * c < p) T[rr * ld + 32 * h + 8 * c + kk] = q.B[w * 4 + c];  // uniform
-            if (h != hs) continue;  // the window's second column chunk is still to come
-            const int qw = g >> hs;
-            if (qw < nr) {  // rectangle rows a .. a + 7 (< m), ascending
-                const int a = p + 8 * qw;
-#pragma unroll
-                for (int u = 0; u < 8; u += 2) {  // x_i broadcast from the lane holding row i
-                    if (a + u < m) {
-                        const int i = a + u;
-                        const double xv = i < 64 ? readlane_d(xr0, i) : readlane_d(xr1, i - 64);
-                        s0 += T[u * ld + lane] * xv;
-                    }
-                    if (a + u + 1 < m) {
-                        const int i = a + u + 1;
-                        const double xv = i < 64 ? readlane_d(xr0, i) : readlane_d(xr1, i - 64);
-                        s1 += T[(u + 1) * ld + lane] * xv;
-                    }
-                }
-                if (qw == nr - 1 && live) xj -= s0 + s1;
-            } else {  // triangle rows k = b - 1 .. a
-                if (qw == 0 && live) xj -= s0 + s1;  // no rectangle rows
-                const int a = 8 * (nt - 1 - (qw - nr));
-                const int b = min(a + 8, p);
-#pragma unroll
-                for (int u = 7; u >= 0; --u) {
-                    const int k = a + u;
-                    if (k < b) {
-                        const double l = T[u * ld + lane];
-                        const double xb = readlane_d(xj, k);
-                        const double xk = (liveM >> k) & 1 ? xb : 0.0;
-                        const int skip = (twoBM >> k) & 1 ? k - 1 : -1;
-                        const double tv = xj - l * xk;
-                        xj = (live && lane < k && lane != skip) ? tv : xj;
-                    }
-                }
+        for (int u = 0; u < 8; ++u) {
+            const int k = kh - u;
+            if (k >= 0) {  // uniform
+                const double xb = readlane_d(xj, k);
+                const double xk = (liveM >> k) & 1 ? xb : 0.0;
+                const int skip = (twoBM >> k) & 1 ? k - 1 : -1;
+                const double tv = xj - lv[u] * xk;
+                xj = (live && lane < k && lane != skip) ? tv : xj;
             }
         }
     }
     return xj;
 }
 
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_bwd_rg(SolveArgs A, DfArgs D) {
+struct RgBwdMeta {
+    int piv;          // lane < p: pivot kind
+    double e0;        // lane < p: z (forward result)
+    int32_t a0;       // p <= lane < m: xs index of row lane (an ancestor's published solution value)
+    int32_t ah;       // m > 64: xs index of row 64 + (lane & 7)
+    uint32_t dep;     // parent's done word as seen at issue time (sc1)
+    double H[4];      // rows 64..71 (compact, see rg_load_high)
+};
+__device__ __forceinline__ void rg_bwd_meta(const SolveArgs& A, const DfArgs& D, const FrontRec& r, RgBwdMeta& q) {
+    const int lane = threadIdx.x;
+    const int m = r.m, p = r.p;
+    const int64_t ro = r.ro;
+    q.piv = lane < p ? (int)A.piv[ro + lane] : (int)PIV_NULL;
+    q.e0 = lane < p ? D.xs[r.woff + lane] : 0.0;
+    q.a0 = lane >= p && lane < m ? D.rxpos[ro + lane] : 0;
+    q.ah = 64 + (lane & 7) < m ? D.rxpos[ro + 64 + (lane & 7)] : 0;
+    q.dep = r.par >= 0 ? ld_sc1_u32(D.done + r.par) : 0u;
+    if (m > 64) rg_load_high(A.L, r.Lo, m, p, q.H);
+}
+
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_solve_bwd_rg(SolveArgs A, DfArgs D) {
     extern __shared__ __attribute__((aligned(16))) double smem_s[];
     const int lane = threadIdx.x;
-    const int G = gridDim.x;
+    const int G = (int)gridDim.x - D.ov_grid;
+    if ((int)blockIdx.x >= G) {  // over role: the oversized fronts' walk, last to first
+        for (int t = blockIdx.x - G; t < D.ov_nf; t += D.ov_grid) {
+            const FrontRec r = df_record(D.ov_desc[(D.ov_nf - 1 - t) * 16 + (lane & 15)]);
+            unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)r.f + 4 : nullptr;
+            if (st && lane == 0) st[0] = st[1] = __builtin_amdgcn_s_memrealtime();
+            rg_bwd_over(A, D, r, smem_s, smem_s + 128);
+            if (st && lane == 0) st[2] = st[3] = __builtin_amdgcn_s_memrealtime();
+        }
+        return;
+    }
     int t = blockIdx.x;
-    if (t >= D.nf) return;
-    double* T = smem_s;         // one 8-row window of L (8 x ld doubles)
-    FrontRec r = df_record(df_desc_load(D, D.nf - 1 - t));
-    RgBwdIn q;
-    rg_bwd_issue(A, D, r, q);
-    int dn = df_desc_load(D, D.nf - 1 - min(t + G, D.nf - 1));
+    if (t >= D.rg_nf) return;
+    double* T = smem_s;  // 32 x 33 doubles
+    const int* desc = D.rg_desc;
+    const int nf = D.rg_nf;
+    FrontRec r = df_record(desc[(nf - 1 - t) * 16 + (lane & 15)]);
+    RgBwdMeta q;
+    double B[kRgCols];
+    rg_bwd_meta(A, D, r, q);
+    rg_load_cols(A.L, r.Lo, r.m, r.p, 0, 0, B);
+    int dn = desc[(nf - 1 - min(t + G, nf - 1)) * 16 + (lane & 15)];
     for (;;) {
         const int m = r.m, p = r.p, f = r.f;
+        const int64_t woff = r.woff;
         unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)f + 4 : nullptr;
         if (st && lane == 0) st[0] = __builtin_amdgcn_s_memrealtime();
-        const unsigned long long liveM = __ballot(lane < p && q.piv != PIV_NULL);
-        const unsigned long long twoBM = __ballot(lane < p && q.piv == PIV_2X2_B);
         if (r.par >= 0 && (int32_t)(q.dep - D.epoch) < 0) df_wait(D.done + r.par, D.epoch, D.abort_flag);
-        // the rows' values in lane = row order: own z (lane < p), the ancestors' published solution values
+        // the rows' values, lane = row: own z (lane < p), the ancestors' published solution values
         const double xr0 = lane < p ? q.e0 : (lane < m ? ld_sc1(D.xs + q.a0) : 0.0);
-        const double xr1 = lane + 64 < m ? ld_sc1(D.xs + q.a1) : 0.0;
+        const double xh = 64 + (lane & 7) < m ? ld_sc1(D.xs + q.ah) : 0.0;
+        const int piv = q.piv;
+        double H[4];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) H[c] = q.H[c];
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
-        const double xj = rg_bwd_front(A, r, q, liveM, twoBM, xr0, xr1, T, q.e0);
-        if (lane < p) st_sc1(D.xs + r.woff + lane, xj);
-        if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         const int tn = t + G;
-        const bool more = tn < D.nf;
-        asm volatile("" ::: "memory");  // the next front's loads are not hoisted above this front's work
-        if (more) {
-            r = df_record(dn);
-            dn = df_desc_load(D, D.nf - 1 - min(tn + G, D.nf - 1));
-            rg_bwd_issue(A, D, r, q);
-        }
+        const bool more = tn < nf;
+        FrontRec rn = r;
+        auto next = [&]() {  // the next front's loads, issued as soon as B is free
+            if (more) {
+                rn = df_record(dn);
+                dn = desc[(nf - 1 - min(tn + G, nf - 1)) * 16 + (lane & 15)];
+                rg_bwd_meta(A, D, rn, q);
+                rg_load_cols(A.L, rn.Lo, rn.m, rn.p, 0, 0, B);
+            }
+        };
+        const double xj = rg_bwd_core(B, H, xr0, xh, m, p, piv, T, next);
+        if (lane < p) st_sc1(D.xs + woff + lane, xj);
+        if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         drain_stores();
         if (lane == 0) __hip_atomic_store(D.done + f, D.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (!more) break;
+        r = rn;
         t = tn;
     }
+}
+
+// level-scheduled backward of one-wave fronts with the arithmetic of k_solve_bwd_rg (w by original index):
+// rg_bwd_core for fronts with p <= 32, m <= 72, the oversized fronts' LDS-panel code otherwise
+__global__ __launch_bounds__(64) void k_solve_bwd_w2(SolveArgs A, const int32_t* __restrict__ fronts) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    const int f = fronts[blockIdx.x];
+    const int m = A.fm[f], p = A.fp[f];
+    const int64_t ro = A.rows_off[f], Lo = A.L_off[f];
+    const int piv = lane < p ? (int)A.piv[ro + lane] : (int)PIV_NULL;
+    double xj;
+    if (rg_fits(m, p)) {
+        double B[kRgCols], H[4];
+        rg_load_cols(A.L, Lo, m, p, 0, 0, B);
+        if (m > 64) rg_load_high(A.L, Lo, m, p, H);
+        const double xr0 = lane < m ? A.w[A.frow[ro + lane]] : 0.0;
+        const double xh = 64 + (lane & 7) < m ? A.w[A.frow[ro + 64 + (lane & 7)]] : 0.0;
+        xj = rg_bwd_core(B, H, xr0, xh, m, p, piv, smem_s, [] {});
+    } else {
+        double* X = smem_s;
+        for (int i = lane; i < m; i += 64) X[i] = A.w[A.frow[ro + i]];
+        xj = rg_bwd_over_core(A.L, Lo, m, p, smem_s + 128, X, piv);
+    }
+    if (lane < p) A.w[A.frow[ro + lane]] = xj;
 }
 
 // right-hand side into elimination order (xs[xpos[i]] = s_i b_i) and the solution back (x_i = s_i xs[xpos[i]])
@@ -3988,17 +4178,21 @@ hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int ld
 
 // register-resident dataflow solve kernels (k_solve_{fwd,bwd}_rg): grid = resident blocks (one below the
 // occupancy query's answer per CU, which can over-report by one), at most the walk length
-static constexpr size_t kRgFwdLds = 128 * sizeof(double) + 128 * sizeof(int32_t);
-static constexpr size_t kRgBwdLds = 8 * kRgLd * sizeof(double);
+static constexpr size_t kRgFwdLds = (192 + (kRgRegion > 8 * 33 ? kRgRegion : 8 * 33)) * sizeof(double);
+static constexpr size_t kRgBwdLds = (32 * 33 > 128 + kRgRegion ? 32 * 33 : 128 + kRgRegion) * sizeof(double);
+static int g_rg_wpe = 3;  // waves per SIMD of the walk kernels' register budget (option "solve_rg_wpe": 3 or 4)
+void set_solve_rg_wpe(int w) { g_rg_wpe = w == 4 ? 4 : 3; }
 int solve_rg_grid(bool forward, int nf) {
-    static int per_cu[2] = {-1, -1}, cus = 0;
-    const int d = forward ? 0 : 1;
+    static int per_cu[4] = {-1, -1, -1, -1}, cus = 0;
+    const int d = (forward ? 0 : 1) + (g_rg_wpe == 4 ? 2 : 0);
     if (per_cu[d] < 0) {
         int dev = 0, n = 0;
         if (hipGetDevice(&dev) != hipSuccess) return 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
-        hipError_t e = forward ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_fwd_rg, 64, kRgFwdLds)
-                               : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_bwd_rg, 64, kRgBwdLds);
+        hipError_t e = d == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_fwd_rg<3>, 64, kRgFwdLds)
+                       : d == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_bwd_rg<3>, 64, kRgBwdLds)
+                       : d == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_fwd_rg<4>, 64, kRgFwdLds)
+                                : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_bwd_rg<4>, 64, kRgBwdLds);
         if (e != hipSuccess) return 0;
         per_cu[d] = n - 1;
     }
@@ -4008,8 +4202,21 @@ int solve_rg_grid(bool forward, int nf) {
 
 hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, hipStream_t s) {
     if (D.nf <= 0 || grid <= 0) return hipSuccess;
-    if (forward) hipLaunchKernelGGL(k_solve_fwd_rg, dim3(grid), dim3(64), kRgFwdLds, s, A, D);
-    else hipLaunchKernelGGL(k_solve_bwd_rg, dim3(grid), dim3(64), kRgBwdLds, s, A, D);
+    if (g_rg_wpe == 4) {
+        if (forward) hipLaunchKernelGGL(k_solve_fwd_rg<4>, dim3(grid), dim3(64), kRgFwdLds, s, A, D);
+        else hipLaunchKernelGGL(k_solve_bwd_rg<4>, dim3(grid), dim3(64), kRgBwdLds, s, A, D);
+    } else {
+        if (forward) hipLaunchKernelGGL(k_solve_fwd_rg<3>, dim3(grid), dim3(64), kRgFwdLds, s, A, D);
+        else hipLaunchKernelGGL(k_solve_bwd_rg<3>, dim3(grid), dim3(64), kRgBwdLds, s, A, D);
+    }
+    return hipGetLastError();
+}
+
+// level-scheduled backward of one-wave fronts through rg_bwd_core (handles whose fronts all have p <= 32,
+// m <= 72: the arithmetic of k_solve_bwd_rg)
+hipError_t launch_solve_bwd_w2(const SolveArgs& A, const int32_t* fronts, int count, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_solve_bwd_w2, dim3(count), dim3(64), kRgBwdLds, s, A, fronts);
     return hipGetLastError();
 }
 

@@ -120,6 +120,10 @@ struct DfArgs {
     uint32_t* abort_flag;       // set when a wait exceeded its limit (result invalid, host falls back)
     int32_t win;                // LDS panel window (doubles, even, >= the longest column); rows follow it
     int32_t piv_off;            // LDS offset (doubles) of the 64 pivot-kind words, after the rows
+    const int32_t* rg_desc;     // register kernels (k_solve_*_rg): the walk's fronts with p <= 32, m <= 72 (16 words each)
+    int32_t rg_nf;
+    const int32_t* ov_desc;     // ... the other fronts, same order, walked by the launch's last ov_grid blocks
+    int32_t ov_nf, ov_grid;
     unsigned long long* stamps; // diagnostics (nullptr in normal runs): per front and direction 4 s_memrealtime
                                 // words {start, dependency satisfied, values staged, published}
 };
@@ -264,6 +268,8 @@ int solve_df_grid(int lds_doubles, int nf);
 int solve_slack_doubles();
 // register-resident dataflow solve (same DfArgs walk and hand-offs as launch_solve_df; p <= 64, m <= 128)
 int solve_rg_grid(bool forward, int nf);
+void set_solve_rg_wpe(int waves_per_simd);  // 3 or 4 (A/B of the walk kernels' register budget)
+hipError_t launch_solve_bwd_w2(const SolveArgs& A, const int32_t* fronts, int count, hipStream_t s);
 hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, hipStream_t s);
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
 // rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch.  Distributed
