@@ -204,15 +204,18 @@ def test_small_dense_fronts(uno_amd):
     assert rel_residual(n, r, c, v, xg, b) < RES_TOL
 
 
-@pytest.mark.parametrize("rg", [0, 1])
+@pytest.mark.parametrize("rg", [0, 1, 2])
 def test_dataflow_solve_kernels_bit_identical(uno_amd, rg):
     """C3-shaped arrowband at N = 1e5 (fronts of up to 72 rows, 2x2 pivots): the dataflow solve kernels
-    (rg = 1: register-resident k_solve_{fwd,bwd}_rg, the default; rg = 0: the LDS-panel k_solve_*_df) give
+    (rg = 1: register-resident k_solve_fwd_rg + LDS-panel k_solve_bwd_df, the default; rg = 2: both register
+    kernels, whose backward sums the rectangle in another order, so the level schedule follows it through
+    k_solve_bwd_w2; rg = 0: the LDS-panel k_solve_*_df) give
     solutions bit-identical to the level-scheduled launches, over repeated solves (the arrival counters'
     epochs) and after a refactorization with new values."""
     from uno_amd import arrowband, SEEDS, HipKKT
     n, nv, m, r, c, v, b = arrowband(100000, SEEDS["C3"])
-    gd, gl = HipKKT(0, solve_rg=rg), HipKKT(0, dataflow_solve=0, solve_rg=rg)
+    opt = dict(solve_rg=int(rg > 0), solve_rg_bwd=int(rg == 2))
+    gd, gl = HipKKT(0, **opt), HipKKT(0, dataflow_solve=0, **opt)
     for g in (gd, gl):
         g.analyze(n, r, c)
         g.factorize(v)

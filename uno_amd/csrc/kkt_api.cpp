@@ -188,7 +188,9 @@ struct uno_kkt {
     int32_t n_df_roots = 0, n_df_topf = 0;
     DBuf<unsigned long long> df_abort64;
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
-    int solve_rg = 1;              // option "solve_rg": register-resident dataflow kernels (k_solve_*_rg)
+    int solve_rg = 1;              // option "solve_rg": register-resident forward walk kernel (k_solve_fwd_rg)
+    int solve_rg_bwd = 0;          // option "solve_rg_bwd": register-resident backward walk (k_solve_bwd_rg; its
+                                   // transpose-reduced rectangle sums in another order, so the level schedule follows)
     int rg_grid_f = 0, rg_grid_b = 0;
     bool rg_fwd_ok = false;        // the walk meets k_solve_fwd_rg's precondition (every front p <= 32, m <= 72)
     bool new_bwd = false;          // option solve_rg: the backward of one-wave fronts runs the register kernels' arithmetic
@@ -920,7 +922,7 @@ void set_rg_grids(uno_kkt_t h) {
 
 hipError_t setup_dataflow(uno_kkt_t h) {
     const Symbolic& S = h->S;
-    h->new_bwd = h->solve_rg != 0;
+    h->new_bwd = h->solve_rg_bwd != 0;
     h->df_grid = 0;
     h->df_rx_valid = false;
     h->df_epoch = 0;
@@ -1554,8 +1556,8 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }
-    else if (n == "solve_rg") {
-        h->solve_rg = value != 0.0;
+    else if (n == "solve_rg" || n == "solve_rg_bwd") {
+        (n == "solve_rg" ? h->solve_rg : h->solve_rg_bwd) = value != 0.0;
         if (h->analyzed) {
             HIPCHK(h, setup_dataflow(h));
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -1798,7 +1800,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
     DfArgs Df;
     auto walk = [&](bool forward) -> hipError_t {
         const int g = forward ? h->rg_grid_f : h->rg_grid_b;
-        if (h->solve_rg && h->rg_fwd_ok && (forward || h->new_bwd) && g > 0) return launch_solve_rg(A, Df, g, forward, s);
+        if (h->rg_fwd_ok && (forward ? h->solve_rg != 0 : h->new_bwd) && g > 0) return launch_solve_rg(A, Df, g, forward, s);
         return launch_solve_df(A, Df, h->df_grid, h->df_lds, forward, s);
     };
     if (df) {

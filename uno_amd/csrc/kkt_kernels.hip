@@ -2549,7 +2549,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         df_issue<true>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         const int mypiv = ipl[lane];
-        fwd_compute_win2(A.L, Lo, m, p, P, D.win, k1, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
+        fwd_compute_win(A.L, Lo, m, p, P, D.win, k1, y, mypiv, D.xs + woff + lane, D.cvx + xoff);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         pend = par;
         __syncthreads();  // LDS reused by the next front
@@ -2600,7 +2600,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         df_issue<false>(A, D, q);
         if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
         const int mypiv = ipl[lane];
-        const double xj = bwd_compute_win2(A.L, Lo, m, p, P, D.win, c0, x, mypiv);
+        const double xj = bwd_compute_win(A.L, Lo, m, p, P, D.win, c0, x, mypiv);
         if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
         if (lane < p) st_sc1(D.xs + woff + lane, xj);
         pend = f;
