@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over the solve kernels (one rocprofv3 --pmc pass each; bench --profile-only): bash tools/r04_pmc_solve.sh TAG [bench args]
+# PMC passes (one rocprofv3 --pmc pass each; bench --profile-only): bash tools/r04_pmc.sh TAG [bench args]; summaries per kernel in gpurun_out/TAG/[abcd].txt
 T=${1:-pmcs}; shift
 export TMPDIR=/tmp
 mkdir -p gpurun_out/$T
@@ -13,4 +13,4 @@ timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/$T/d
 for p in a b c d; do
   [ -f gpurun_out/$T/$p/run_results.db ] && python tools/rocpd_summary.py bykernel gpurun_out/$T/$p/run_results.db > gpurun_out/$T/$p.txt 2>&1
 done
-grep -h -A9 "k_solve" gpurun_out/$T/[abcd].txt | head -120
+grep -h -A9 -E "${PMC_GREP:-k_solve}" gpurun_out/$T/[abcd].txt | head -${PMC_LINES:-120}

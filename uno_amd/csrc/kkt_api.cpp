@@ -140,7 +140,7 @@ struct uno_kkt {
     const double* values_ptr = nullptr;  // device values used by the last factorization
     // device arrays
     DBuf<double> values, uval, scale, L, cb, gscratch, w, cvec, rowsum, rmax, bvec;
-    DBuf<int32_t> slot_src;               // k_pack: per slot its single COO position, or -1 (multi_slots)
+    DBuf<int32_t> slot_src;               // k_pack: per slot its single COO position, or -1 - (multi_slots record)
     DBuf<int32_t> multi_slots;            // slots with several COO positions (k_pack_multi)
     int64_t n_multi = 0;
     DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, fstat;
@@ -217,10 +217,13 @@ struct uno_kkt {
     hipEvent_t ev_counters = nullptr;  // after the counters' read-back of the last enqueued factorization
     hipEvent_t ev_wait = nullptr;      // host_wait_stream
     int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
-    bool rmax_clean = false;           // rmax all zero (left so by the front sweeps)
+    DBuf<unsigned long long> rmaxk;    // front sweeps: n row maxima per sweep (elimination order)
+    DBuf<int32_t> rows_sw;             // front sweeps: the fronts' rows in the elimination order
+    DBuf<int8_t> longpos_sw;           // front sweeps: longpos by new index
+    DBuf<int32_t> long_sw;             // front sweeps: the long rows' new indices
+    bool rmaxk_clean = false;          // rmaxk all zero (left so by k_sweep_final)
     int front_scale = 0;         // option "front_scale": the scaling gathered per front row (k_front_scale) for the
-                                 // factorization (1), also before every sweep (2)
-    int sweep_coalesced = 1;     // option "sweep_coalesced"
+                                 // factorization (1; 2 is accepted as 1)
     DBuf<double> fscale;
     DBuf<int8_t> flong;          // per front row: index of its row among the long rows, -1 otherwise
     int dff_enabled = 1;  // 0 off, 1 (default) levels >= L*, 2 also the small fronts below them (measured no faster at C3)
@@ -1066,7 +1069,7 @@ int upload_structure(uno_kkt_t h) {
         std::vector<int32_t> src((size_t)S.nu), multi;
         for (int64_t e = 0; e < S.nu; ++e) {
             const int32_t q0 = S.dup_ptr[e], cnt = S.dup_ptr[e + 1] - q0;
-            src[e] = cnt == 1 ? S.dup_pos[q0] : -1;
+            src[e] = cnt == 1 ? S.dup_pos[q0] : -1 - (int32_t)(multi.size() / 4);  // < 0: its multi record
             if (cnt == 1) continue;
             multi.push_back((int32_t)e);
             if (cnt <= 3) {
@@ -1155,6 +1158,16 @@ int upload_structure(uno_kkt_t h) {
             if (lr.size() > 127) h->use_front_sweeps = false;  // int8 index
             HIPCHK(h, h->longpos.upload(lp, s));
             HIPCHK(h, h->long_orig.upload(lo, s));
+            {  // the sweeps index rows in the elimination order (a front's rows are then clustered: the
+               // scaling gathers and row-maximum atomics touch fewer cache lines than by original id)
+                std::vector<int8_t> lpn((size_t)std::max<int64_t>(n, 1), (int8_t)-1);
+                for (size_t k = 0; k < lr.size(); ++k) lpn[lr[k]] = (int8_t)k;
+                std::vector<int32_t> rn(std::max<size_t>(S.rows.size(), 1), 0);
+                for (size_t t = 0; t < S.rows.size(); ++t) rn[t] = S.iperm[S.rows[t]];
+                HIPCHK(h, h->longpos_sw.upload(lpn, s));
+                HIPCHK(h, h->long_sw.upload(lr, s));
+                HIPCHK(h, h->rows_sw.upload(rn, s));
+            }
             {  // the same per front row (the sweeps read it with the row ids, no dependent gather)
                 std::vector<int8_t> fl(std::max<size_t>(S.rows.size(), 1), (int8_t)-1);
                 for (size_t t = 0; t < S.rows.size(); ++t) fl[t] = lp[S.rows[t]];
@@ -1181,7 +1194,6 @@ int upload_structure(uno_kkt_t h) {
         if (n > 0) HIPCHK(h, hipMemsetAsync(h->scale.p, 0, sizeof(double) * n, s));  // rows of other ranks: x = 0
         HIPCHK(h, h->rowsum.alloc(n));
         HIPCHK(h, h->rmax.alloc(n));
-        h->rmax_clean = false;
         HIPCHK(h, h->w.alloc(n));
         HIPCHK(h, h->bvec.alloc(n));
         HIPCHK(h, h->xtmp.alloc(n));
@@ -1284,23 +1296,26 @@ int enqueue_factorization(uno_kkt_t h) {
         SA.scale_in = h->w.p;      // (free until the solve)
         h->scan = SA;
         h->norm_valid = false;
-        if (!h->use_front_sweeps) h->rmax_clean = false;  // the paths below use rmax as scratch
         if (h->use_front_sweeps) {
             SweepArgs W;
-            W.nf = S.nf; W.n = S.n; W.fm = h->fm.p; W.rows_off = h->rows_off.p; W.rows = h->rows.p;
+            W.nf = S.nf; W.n = S.n; W.fm = h->fm.p; W.rows_off = h->rows_off.p; W.rows = h->rows_sw.p;
+            W.perm = h->perm_d.p;
             W.ent_off = h->ent_off.p; W.ent_lpos = h->ent_lpos.p; W.values = h->values_ptr; W.dup_ptr = h->dup_ptr.p;
             W.dup_pos = h->dup_pos.p; W.slot_src = h->slot_src.p; W.uval = h->uval.p;
             W.multi = h->multi_slots.p; W.n_multi = h->n_multi; W.scale = h->scale.p; W.ent_total = S.nu;
-            W.rmax = reinterpret_cast<unsigned long long*>(h->rmax.p); W.longpos = h->longpos.p;
-            W.long_orig = h->long_orig.p; W.n_long = h->n_long; W.part_long = h->part_long.p; W.max_m = (int)S.max_m;
+            const size_t need = (size_t)S.n * std::max(h->scale_iters, 1);
+            if (h->rmaxk.n != need) {
+                HIPCHK(h, h->rmaxk.alloc(need));
+                h->rmaxk_clean = false;
+            }
+            W.rmax_all = h->rmaxk.p; W.rmax = h->rmaxk.p; W.longpos = h->longpos_sw.p;
+            W.long_orig = h->long_sw.p; W.n_long = h->n_long; W.part_long = h->part_long.p; W.max_m = (int)S.max_m;
             W.big_list = h->sweep_big.p; W.n_big = h->n_sweep_big; W.big_slices = h->sweep_slices;
-            W.fscale = h->front_scale == 2 ? h->fscale.p : nullptr;  // measured slower: 3 extra gathers (r03)
-            W.coalesced = h->sweep_coalesced;
             W.rows_total = (int64_t)S.rows.size();
             W.flong = h->n_long > 0 ? h->flong.p : nullptr;
-            W.rmax_zero = h->rmax_clean;
+            W.rmax_zero = h->rmaxk_clean;
             HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
-            h->rmax_clean = true;  // the last k_sweep_update cleared it
+            h->rmaxk_clean = true;  // k_sweep_final cleared it
             if (h->overlap_norm && !h->exact_next) {
                 h->last_optimistic = true;  // row sums only if a pivot is small (sync_and_verify)
             } else {
@@ -1323,8 +1338,8 @@ int enqueue_factorization(uno_kkt_t h) {
             if (rc != UNO_KKT_OK) return rc;
         }
     }
-    // the scaling per front row (the front sweeps leave it gathered after their last update)
-    if (h->front_scale && !(h->use_front_sweeps && h->scale_iters > 0 && h->front_scale == 2))
+    // the scaling per front row
+    if (h->front_scale)
         HIPCHK(h, launch_front_scale(h->rows.p, h->scale.p, h->fscale.p, (int64_t)S.rows.size(), s));
     FactorArgs A;
     A.fscale = h->front_scale ? h->fscale.p : nullptr;
@@ -1531,7 +1546,6 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "early_xpos") h->early_xpos = value != 0.0;
     else if (n == "spin_wait") h->spin_wait = value != 0.0;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
-    else if (n == "sweep_coalesced") h->sweep_coalesced = value != 0.0;
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;
     else if (n == "dist_force") h->dist_force = value != 0.0;

@@ -451,8 +451,43 @@ __global__ __launch_bounds__(256) void k_rowscanR(ScanArgs A) {
 // milliseconds: grid (big fronts x slices) of 256-thread blocks, each reducing a slice of the slots into
 // its LDS row maxima, one atomic max per (block, row) straight into rmax (long rows included: there are
 // few such blocks).  The one-wave launch skips those fronts (their long-row partials stay 0).
+// a slot with several COO positions (k_pack_multi's record): duplicates summed in ascending COO position
+__device__ __forceinline__ double pack_multi_value(const double* __restrict__ values, const int32_t* __restrict__ dup_pos,
+                                                   int4 d) {
+    double v = 0.0;
+    if (d.y >= -1) {
+        const double a = values[d.y], b = d.z >= 0 ? values[d.z] : 0.0, c = d.w >= 0 ? values[d.w] : 0.0;
+        v += a;
+        if (d.z >= 0) v += b;
+        if (d.w >= 0) v += c;
+    } else {
+        for (int32_t q = -2 - d.y; q < -2 - d.y + d.z; ++q) v += values[dup_pos[q]];
+    }
+    return v;
+}
+
+// the scaling of row r before sweep A.iter: s = 1, then s <- s / sqrt(rmax_j(r)) for every earlier sweep j
+// with rmax_j(r) > 0 (k_sweep_final's expression, so every sweep and the final scaling agree to the bit).
+// The sweeps' row maxima stay in separate buffers until k_sweep_final: no update kernel between sweeps.
+__device__ __forceinline__ double sweep_row_scale(const SweepArgs& A, int32_t r) {
+    double x[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) x[j] = j < A.iter ? as_double(A.rmax_all[(int64_t)j * A.n + r]) : 0.0;
+    double s = 1.0;
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+        if (x[j] > 0.0) s = s / sqrt(x[j]);
+    for (int j = 3; j < A.iter; ++j) {
+        const double y = as_double(A.rmax_all[(int64_t)j * A.n + r]);
+        if (y > 0.0) s = s / sqrt(y);
+    }
+    return s;
+}
+
+// 8 waves per SIMD (<= 64 VGPRs): the one-wave fronts are latency-bound, occupancy pays (76 VGPRs, 6 waves:
+// 0.360 ms scale phase at C3; 54 VGPRs, 8 waves: 0.337 ms)
 template <bool FIRST, bool BIG>
-__global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k_sweep_front(SweepArgs A) {
     extern __shared__ __attribute__((aligned(16))) double swm[];
     const int f = BIG ? A.big_list[blockIdx.x] : blockIdx.x;
     const int m = A.fm[f];
@@ -468,29 +503,54 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
         e0 += chunk * blockIdx.y;
         e1 = e0 + chunk < e1 ? e0 + chunk : e1;
     }
-    // A batch is EB x NT consecutive slots.  Coalesced (default): load u of lane l reads slot base + u NT + l,
-    // so a wave's load instruction covers 256 / 512 contiguous bytes, and every slot does one LDS atomic max
-    // for its row and one for its column.  Otherwise (option sweep_coalesced = 0) each lane takes EB
-    // consecutive slots, keeping its column maximum in a register (one LDS atomic per column run), but each
-    // load instruction then spans NT strided cache lines: 8x the address-unit requests per slot.
+    // A batch is EB x NT consecutive slots: load u of lane l reads slot base + u NT + l, so a wave's load
+    // instruction covers 256 / 512 contiguous bytes, and every slot does one LDS atomic max for its row and
+    // one for its column.  (Each lane taking EB consecutive slots, keeping its column maximum in a register,
+    // measured slower: every load instruction then spans NT strided cache lines.)
     constexpr int EB = 8;
-    const bool coal = A.coalesced != 0;
     uint32_t lp[EB];
     double v[EB];
     auto load = [&](int64_t base) {
+        if (FIRST) {
+            // the pack (k_pack / k_pack_multi semantics) fused into the first sweep: each slot's value from
+            // the caller's COO array, written to uval here
+            int32_t src[EB];
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                const int64_t e = base + (int64_t)u * NT + lane;
+                const bool ok = e < e1;
+                lp[u] = ok ? A.ent_lpos[e] : 0xffffffffu;
+                src[u] = ok ? (A.slot_src != nullptr ? A.slot_src[e] : A.dup_pos[e]) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < EB; ++u) {
+                if (lp[u] == 0xffffffffu) { v[u] = 0.0; continue; }
+                const int64_t e = base + (int64_t)u * NT + lane;
+                double x;
+                if (A.dup_ptr == nullptr) {
+                    x = A.values[src[u]];
+                } else if (src[u] >= 0) {
+                    x = 0.0 + A.values[src[u]];  // as the summed form: -0.0 packs as +0.0
+                } else {
+                    x = pack_multi_value(A.values, A.dup_pos, reinterpret_cast<const int4*>(A.multi)[-1 - src[u]]);
+                }
+                v[u] = x;
+                A.uval[e] = x;
+            }
+            return;
+        }
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-            const int64_t e = coal ? base + (int64_t)u * NT + lane : base + (int64_t)lane * EB + u;
+            const int64_t e = base + (int64_t)u * NT + lane;
             const bool ok = e < e1;
             lp[u] = ok ? A.ent_lpos[e] : 0xffffffffu;
             v[u] = ok ? A.uval[e] : 0.0;
         }
     };
     load(e0);  // the first batch is in flight while the rows' scalings are gathered
-    // one-wave fronts of <= 128 rows keep their row ids and long-row indices in registers for the final
-    // flush, and read the rows' scalings from the per-front-row copy (fscale, gathered after the previous
-    // sweep's update): every load of the front is issued in the first round trip (no rows -> scale or
-    // rows -> longpos chain)
+    // one-wave fronts of <= 128 rows keep their row ids and long-row indices (per-front-row copy flong: no
+    // rows -> longpos chain) in registers for the final flush; the rows' scalings come from the earlier
+    // sweeps' row maxima (sweep_row_scale)
     constexpr int RQ = 2;
     const bool regrows = !BIG && m <= 64 * RQ;
     int32_t rr[RQ];
@@ -504,7 +564,7 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
             rr[u] = ok ? A.rows[ro + q] : 0;
             lk[u] = ok && A.flong ? (int)A.flong[ro + q] : -1;
             sv[u] = 1.0;
-            if (!FIRST && ok) sv[u] = A.fscale ? A.fscale[ro + q] : A.scale[rr[u]];
+            if (!FIRST && ok) sv[u] = sweep_row_scale(A, rr[u]);
         }
 #pragma unroll
         for (int u = 0; u < RQ; ++u) {
@@ -517,11 +577,11 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
     } else {
         for (int q = lane; q < m; q += NT) {
             rm[q] = 0ull;
-            if (!FIRST) sl[q] = A.scale[A.rows[ro + q]];
+            if (!FIRST) sl[q] = sweep_row_scale(A, A.rows[ro + q]);
         }
     }
     __syncthreads();
-    for (int64_t base = e0; coal;) {
+    for (int64_t base = e0;;) {
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
             if (lp[u] == 0xffffffffu) continue;  // beyond the slot range
@@ -535,33 +595,6 @@ __global__ __launch_bounds__(256) void k_sweep_front(SweepArgs A) {
             atomicMax(rm + lr, bw);
             atomicMax(rm + lc, bw);
         }
-        base += (int64_t)EB * NT;
-        if (base >= e1) break;  // uniform
-        load(base);
-    }
-    for (int64_t base = e0; !coal;) {
-        int cc = -1;
-        unsigned long long cm = 0ull;
-#pragma unroll
-        for (int u = 0; u < EB; ++u) {
-            if (lp[u] == 0xffffffffu) break;  // beyond the slot range (the rest of the lane's chunk too)
-            const int lr = (int)(lp[u] >> 16), lc = (int)(lp[u] & 0x7fffu);
-            double w = fabs(v[u]);
-            if (!FIRST) {
-                const double sr = sl[lr], sc = sl[lc];
-                w = (lp[u] & 0x8000u) ? sc * w * sr : sr * w * sc;
-            }
-            const unsigned long long bw = as_bits(w);
-            atomicMax(rm + lr, bw);
-            if (lc != cc) {
-                if (cc >= 0) atomicMax(rm + cc, cm);
-                cc = lc;
-                cm = bw;
-            } else {
-                cm = cm > bw ? cm : bw;
-            }
-        }
-        if (cc >= 0) atomicMax(rm + cc, cm);
         base += (int64_t)EB * NT;
         if (base >= e1) break;  // uniform
         load(base);
@@ -608,6 +641,22 @@ __global__ __launch_bounds__(256) void k_sweep_long_fin(SweepArgs A) {
     __syncthreads();
     for (int k = threadIdx.x; k < A.n_long; k += 256)
         if (lred[k] != 0ull) atomicMax(A.rmax + A.long_orig[k], lred[k]);
+}
+
+// after the front sweeps: scale (by original id perm[i]) = sweep_row_scale of new index i over all `iters`
+// sweeps, and every sweep's row maxima back to 0 for the next factorization (`passes` buffers: iters == 0
+// still ran the packing pass)
+__global__ void k_sweep_final(unsigned long long* __restrict__ rmax_all, double* __restrict__ scale,
+                              const int32_t* __restrict__ perm, int64_t n, int iters, int passes) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double s = 1.0;
+        for (int j = 0; j < passes; ++j) {
+            const double r = as_double(rmax_all[(int64_t)j * n + i]);
+            if (j < iters && r > 0.0) s = s / sqrt(r);
+            rmax_all[(int64_t)j * n + i] = 0ull;
+        }
+        scale[perm[i]] = s;
+    }
 }
 
 // s <- s / sqrt(r) (s = 1 before the first sweep; rows without entries keep s), and r <- 0 for the next sweep
@@ -2625,7 +2674,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
 //  Both walks issue the next front's loads before draining the finished front's stores, so a front in
 //  the bulk of the tree costs one memory round trip (plus one for its children's / ancestors' values).
 constexpr int kRgCols = 32;   // forward: columns of L per register round
-constexpr int kRgSlots = 32;  // backward: 8-row x 8-column window pieces per register round
 
 // base[rel] with rel clamped into [0, n): a uniform 64-bit base plus a 32-bit byte offset (one VGPR per
 // address: the loads use the scalar-base addressing form)
@@ -3905,15 +3953,13 @@ hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
     SweepArgs A = A0;
     const size_t sh = 16 * (size_t)std::max(A.max_m, 1);
     const dim3 gn(grid_for(A.n, 256));
-    hipError_t e = A.rmax_zero ? hipSuccess : hipMemsetAsync(A.rmax, 0, sizeof(unsigned long long) * A.n, s);
+    const int passes = iters > 0 ? iters : 1;  // iters == 0: one pass packs the values (scaling 1)
+    hipError_t e = A.rmax_zero ? hipSuccess : hipMemsetAsync(A.rmax_all, 0, sizeof(unsigned long long) * A.n * passes, s);
     if (e != hipSuccess) return e;
-    if (A.nf > 0) {  // COO values -> packed slots (duplicates summed)
-        e = launch_pack(A.values, A.dup_ptr, A.dup_pos, A.slot_src, 0, A.ent_total, A.uval, s);
-        if (e != hipSuccess) return e;
-        if (A.slot_src != nullptr) e = launch_pack_multi(A.values, A.dup_ptr, A.dup_pos, A.multi, A.n_multi, A.uval, s);
-        if (e != hipSuccess) return e;
-    }
-    for (int it = 0; it < (iters > 0 ? iters : 1); ++it) {
+    // the COO values are packed into the slots by the first sweep (k_sweep_front<true, .>)
+    for (int it = 0; it < passes; ++it) {
+        A.iter = it;
+        A.rmax = A.rmax_all + (int64_t)it * A.n;
         if (A.nf > 0) {
             if (it == 0) hipLaunchKernelGGL((k_sweep_front<true, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
             else hipLaunchKernelGGL((k_sweep_front<false, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
@@ -3927,14 +3973,8 @@ hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
             const unsigned gl = (unsigned)std::min<int64_t>(256, (A.nf + 255) / 256);
             hipLaunchKernelGGL(k_sweep_long_fin, dim3(std::max(gl, 1u)), dim3(256), sizeof(unsigned long long) * A.n_long, s, A);
         }
-        hipLaunchKernelGGL(k_sweep_update, gn, dim3(256), 0, s, A.rmax, A.scale, A.n, it == 0 ? 1 : 0);
-        // the scaling per front row for the next sweep (and, after the last one, for the factorization)
-        if (A.fscale) {
-            e = launch_front_scale(A.rows, A.scale, A.fscale, A.rows_total, s);
-            if (e != hipSuccess) return e;
-        }
     }
-    if (iters == 0) hipLaunchKernelGGL(k_fill_ones, gn, dim3(256), 0, s, A.scale, A.n);  // the pass above only packed
+    hipLaunchKernelGGL(k_sweep_final, gn, dim3(256), 0, s, A.rmax_all, A.scale, A.perm, A.n, iters, passes);
     return hipGetLastError();
 }
 

@@ -163,31 +163,32 @@ struct SweepArgs {
     int64_t nf, n;
     const int32_t* fm;
     const int64_t* rows_off;
-    const int32_t* rows;        // original ids
+    const int32_t* rows;        // the fronts' rows, by new index (elimination order: rmax_all, longpos, long_orig too)
+    const int32_t* perm;        // new index -> original id (k_sweep_final writes scale by original id)
     const int64_t* ent_off;     // nf+1 slot ranges
     const uint32_t* ent_lpos;   // (lr << 16) | flip << 15 | lc
     const double* values;       // caller's COO values (packed into uval by k_pack first)
     int64_t ent_total;          // packed slots
     const int32_t* dup_ptr;     // nullptr: one COO position per slot
     const int32_t* dup_pos;
-    const int32_t* slot_src;    // k_pack: single COO position per slot, < 0: in `multi` (k_pack_multi)
+    const int32_t* slot_src;    // single COO position per slot; < 0: record -1 - slot_src of `multi`
     const int32_t* multi;       // slots with several COO positions
     int64_t n_multi;
     double* uval;
-    double* scale;              // by original id
-    unsigned long long* rmax;   // n, zero between sweeps
-    const int8_t* longpos;      // by original id: index among the long rows, -1 otherwise
-    const int32_t* long_orig;   // n_long original ids
+    double* scale;              // by original id (written after the last sweep)
+    unsigned long long* rmax_all;  // n per sweep (max(iters, 1) buffers), all zero on entry (left so on exit)
+    unsigned long long* rmax;   // launch_front_sweeps: this sweep's buffer in rmax_all
+    int iter = 0;               // launch_front_sweeps: this sweep's index
+    const int8_t* longpos;      // by new index: index among the long rows, -1 otherwise
+    const int32_t* long_orig;   // n_long new indices
     int32_t n_long;
     double* part_long;          // nf * n_long
     int max_m;
-    int coalesced = 1;          // slot loads lane-contiguous (see k_sweep_front)
-    double* fscale = nullptr;   // per front row (layout of rows): scale[rows[t]], refreshed after every sweep
-    int64_t rows_total = 0;     // front rows (length of rows / fscale / flong)
+    int64_t rows_total = 0;     // front rows (length of rows / flong)
     const int8_t* flong = nullptr;  // per front row: longpos of its row (-1: not a long row); nullptr: no long rows
     const int32_t* big_list;    // fronts of more than kSweepBigSlots slots (swept by 2-D grids)
     int32_t n_big = 0, big_slices = 1;
-    int rmax_zero = 0;  // rmax is known to be all zero (k_sweep_update leaves it so): no clearing memset
+    int rmax_zero = 0;  // rmax_all is known to be all zero (k_sweep_final leaves it so): no clearing memset
 };
 hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s);
 hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
