@@ -106,6 +106,17 @@ int uno_kkt_factorize(uno_kkt_t handle, const double* values, int values_on_devi
  * each of which unregisters it). */
 int uno_kkt_factorize_update(uno_kkt_t handle, const double* values, int64_t first, int64_t count);
 
+/* Staged upload while the caller assembles: copies host values [first, first + count) of
+ * the COO array (analysed order) to the solver's device copy on an upload stream, asynchronously, so
+ * PCIe transfers overlap the caller's assembly of the later entries; the next uno_kkt_factorize(h, NULL, 0)
+ * waits for every staged chunk on the device (no host sync) and factors the device copy.  Chunks of one
+ * set of values may come in any order and may be re-staged (e.g. the regularization diagonal after
+ * COOFormat::set_regularization).  The host buffer stays valid until that factorization has been queried
+ * (uno_kkt_inertia); with option "pin_host_values" it is page-locked like uno_kkt_factorize's.  One-GPU
+ * handles.  Used by the plugin's StagedCOOMatrix (integration/StagedCOOMatrix.hpp); it replaces the whole
+ * upload at the start of MUMPS JOB=2 (MUMPSSolver.cpp:85-89). */
+int uno_kkt_stage_values(uno_kkt_t handle, const double* values, int64_t first, int64_t count);
+
 /* Device-side value edits between factorizations (the inertia-correction loop changes only the
  * regularization diagonal: COOFormat::set_regularization, COOFormat.hpp:102-110). */
 int uno_kkt_set_values(uno_kkt_t handle, const int64_t* positions, const double* values, int64_t count);

@@ -43,12 +43,15 @@ namespace uno {
          return uno_kkt_inertia(static_cast<uno_kkt_t>(h), p, q, z);
       }
       int hip_solve(void* h, const double* b, double* x) { return uno_kkt_solve(static_cast<uno_kkt_t>(h), b, x, 0); }
+      int hip_stage(void* h, const double* v, int64_t first, int64_t count) {
+         return uno_kkt_stage_values(static_cast<uno_kkt_t>(h), v, first, count);
+      }
       const char* hip_last_error(void* h) { return uno_kkt_last_error(static_cast<uno_kkt_t>(h)); }
    } // namespace
 
    const KKTBackend& hip_kkt_backend() {
       static const KKTBackend backend{"HIPLDL", hip_create, hip_destroy, hip_analyze, hip_factorize, hip_factorize_update,
-         hip_inertia, hip_solve, hip_last_error};
+         hip_inertia, hip_solve, hip_last_error, hip_stage};
       return backend;
    }
 
@@ -84,8 +87,7 @@ namespace uno {
       this->objective_gradient.resize(number_variables);
       this->constraints.resize(number_constraints);
       this->constraint_jacobian.resize(number_constraints, number_variables);
-      this->augmented_matrix = SparseSymmetricMatrix<COOFormat<size_t, double>>(this->dimension, number_hessian_nonzeros,
-         regularization_size);
+      this->augmented_matrix = StagedCOOMatrix(this->dimension, number_hessian_nonzeros, regularization_size);
       this->rhs.resize(this->dimension);
       this->solution.resize(this->dimension);
    }
@@ -102,6 +104,18 @@ namespace uno {
       this->analysed_nonzeros = matrix.number_nonzeros();
       this->check(this->backend.analyze(this->handle, static_cast<int64_t>(matrix.dimension()),
          static_cast<int64_t>(this->row_indices.size()), this->row_indices.data(), this->column_indices.data()), "analyze");
+      // from now on the plugin's matrix streams its values to the device as Uno inserts them (chunks of
+      // 2^20 entries = 8 MB): the factorization only waits for the last chunk (StagedCOOMatrix.hpp)
+      const char* env = std::getenv("UNO_HIPLDL_STAGE");
+      const bool stage = this->backend.stage != nullptr && &matrix == &this->augmented_matrix && (env == nullptr || std::atoi(env) != 0);
+      if (stage) {
+         this->augmented_matrix.set_stager([this](const double* values, size_t first, size_t count) {
+            this->check(this->backend.stage(this->handle, values, static_cast<int64_t>(first), static_cast<int64_t>(count)), "stage");
+         }, size_t(1) << 20);
+      }
+      else {
+         this->augmented_matrix.set_stager({}, 1);
+      }
    }
 
    // MUMPSSolver.cpp:85-89 (JOB=2): values straight from the COO storage, no copy on the host
@@ -116,6 +130,10 @@ namespace uno {
       if (retry) {
          this->check(this->backend.factorize_update(this->handle, matrix.data_pointer(), 0,
             static_cast<int64_t>(this->regularization_size)), "factorize");
+      }
+      else if (&matrix == &this->augmented_matrix && this->augmented_matrix.staging()) {
+         this->augmented_matrix.flush();  // the tail (and the regularization diagonal) after the staged chunks
+         this->check(this->backend.factorize(this->handle, nullptr), "factorize");
       }
       else {
          this->check(this->backend.factorize(this->handle, matrix.data_pointer()), "factorize");

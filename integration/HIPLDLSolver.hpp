@@ -18,6 +18,7 @@
 #include "linear_algebra/SparseSymmetricMatrix.hpp"
 #include "linear_algebra/SparseVector.hpp"
 #include "linear_algebra/Vector.hpp"
+#include "StagedCOOMatrix.hpp"
 #include "uno_kkt.h"
 
 namespace uno {
@@ -34,6 +35,9 @@ namespace uno {
       int (*inertia)(void* handle, int64_t* positive, int64_t* negative, int64_t* zero);
       int (*solve)(void* handle, const double* rhs, double* x);
       const char* (*last_error)(void* handle);
+      // optional: asynchronous upload of values[first, first + count) while the caller assembles the rest;
+      // factorize(handle, nullptr) then factors the staged values (nullptr: no staging, host-pointer path)
+      int (*stage)(void* handle, const double* values, int64_t first, int64_t count){nullptr};
    };
    const KKTBackend& hip_kkt_backend();
 
@@ -81,8 +85,8 @@ namespace uno {
       std::vector<double> constraints;
       RectangularMatrix<double> constraint_jacobian;
 
-      // augmented system
-      SparseSymmetricMatrix<COOFormat<size_t, double>> augmented_matrix{};
+      // augmented system: COOFormat semantics, values staged to the device during the assembly
+      StagedCOOMatrix augmented_matrix{};
       Vector<double> rhs{};
       Vector<double> solution{};
 

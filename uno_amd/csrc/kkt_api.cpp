@@ -111,6 +111,11 @@ struct uno_kkt {
     // stream3 beside the first (fork / join events), so one launch's tail overlaps the other's body
     hipStream_t stream3 = nullptr;
     hipStream_t stream4 = nullptr;   // third class stream (option concurrent_classes = 3)
+    // uno_kkt_stage_values: host -> device value chunks while the caller is still assembling (created on
+    // first use); the next uno_kkt_factorize(NULL) makes the solver's stream wait for them
+    hipStream_t upload = nullptr;
+    hipEvent_t ev_upload = nullptr, ev_upload_dep = nullptr;
+    bool staged_pending = false;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_join4 = nullptr;
     hipEvent_t ev_scale = nullptr, ev_norm = nullptr;
     int overlap_norm = 1;
@@ -1514,6 +1519,9 @@ void uno_kkt_destroy(uno_kkt_t h) {
     if (h->ev_join) hipEventDestroy(h->ev_join);
     if (h->ev_join4) hipEventDestroy(h->ev_join4);
     if (h->stream4) { hipStreamSynchronize(h->stream4); hipStreamDestroy(h->stream4); }
+    if (h->upload) { hipStreamSynchronize(h->upload); hipStreamDestroy(h->upload); }
+    if (h->ev_upload) hipEventDestroy(h->ev_upload);
+    if (h->ev_upload_dep) hipEventDestroy(h->ev_upload_dep);
     delete h->comm;
     if (h->stream) hipStreamDestroy(h->stream);
     delete h;
@@ -1640,6 +1648,8 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
                         (long long)Pt.n_subtrees, h->comm_world, h->dist_efficiency, h->dist_min_eff);
         }
     }
+    if (h->upload) HIPCHK(h, hipStreamSynchronize(h->upload));  // staged chunks of the previous pattern
+    h->staged_pending = false;
     HIPCHK(h, h->values.alloc(nnz));
     int rc = upload_structure(h);
     if (rc != UNO_KKT_OK) return rc;
@@ -1697,6 +1707,22 @@ __global__ void k_fill(double* p, int64_t n, double v) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) p[i] = v;
 }
 
+// option pin_host_values: the caller's buffer is page-locked once (hipHostRegister) so every later upload
+// is a direct DMA; it is unregistered when the pointer changes or the handle is destroyed (a registration is
+// keyed by pointer AND length: the same address with another pattern size is a new buffer).  The caller keeps
+// a registered buffer allocated until it passes another pointer, calls uno_kkt_analyze again or destroys the
+// handle (include/uno_kkt.h).
+static void pin_host_buffer(uno_kkt_t h, const double* values) {
+    const int64_t nnz = h->S.nnz;
+    if (!h->pin_host || nnz <= 0) return;
+    if (values == h->pinned_ptr && h->pinned_bytes == (size_t)nnz * sizeof(double)) return;
+    if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
+    h->pinned_bytes = (size_t)nnz * sizeof(double);
+    h->pinned_ptr = hipHostRegister(const_cast<double*>(values), h->pinned_bytes, hipHostRegisterDefault) == hipSuccess
+                        ? values : nullptr;
+    (void)hipGetLastError();
+}
+
 extern "C" {
 
 int uno_kkt_fill_values(uno_kkt_t h, int64_t first, int64_t count, double value) {
@@ -1731,6 +1757,35 @@ int uno_kkt_factorize_update(uno_kkt_t h, const double* values, int64_t first, i
     return uno_kkt_factorize(h, nullptr, 0);
 }
 
+int uno_kkt_stage_values(uno_kkt_t h, const double* values, int64_t first, int64_t count) {
+    if (!h || !values) return UNO_KKT_ERR_ARG;
+    if (!h->analyzed) return set_err(h, UNO_KKT_ERR_STATE, "stage_values before analyze");
+    if (h->world != 1) return set_err(h, UNO_KKT_ERR_STATE, "stage_values: one-GPU handles only");
+    if (first < 0 || count < 0 || first + count > h->S.nnz) return set_err(h, UNO_KKT_ERR_ARG, "range out of bounds");
+    if (count == 0) return UNO_KKT_OK;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (!h->upload) {
+        HIPCHK(h, hipStreamCreateWithFlags(&h->upload, hipStreamNonBlocking));
+        HIPCHK(h, hipEventCreateWithFlags(&h->ev_upload, hipEventDisableTiming));
+        HIPCHK(h, hipEventCreateWithFlags(&h->ev_upload_dep, hipEventDisableTiming));
+    }
+    if (!h->staged_pending) {
+        // first chunk of a new set of values: the work queued so far (a factorization whose redos re-pack
+        // from the device copy, a refined solve whose residual reads it) must be done with the old copy
+        if (h->factor_enqueued) {
+            const int rc = finish_factorization(h);
+            if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
+        }
+        HIPCHK(h, hipEventRecord(h->ev_upload_dep, h->stream));
+        HIPCHK(h, hipStreamWaitEvent(h->upload, h->ev_upload_dep, 0));
+        h->staged_pending = true;
+        h->packed_valid = false;
+    }
+    pin_host_buffer(h, values);
+    HIPCHK(h, hipMemcpyAsync(h->values.p + first, values + first, count * sizeof(double), hipMemcpyHostToDevice, h->upload));
+    return UNO_KKT_OK;
+}
+
 int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
     if (!h) return UNO_KKT_ERR_ARG;
     if (!h->analyzed) return set_err(h, UNO_KKT_ERR_STATE, "factorize before analyze");
@@ -1743,23 +1798,18 @@ int uno_kkt_factorize(uno_kkt_t h, const double* values, int values_on_device) {
         if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
     }
     h->factored = false;
+    if (h->staged_pending) {  // chunks of uno_kkt_stage_values: the solver's stream waits for the last one
+        HIPCHK(h, hipEventRecord(h->ev_upload, h->upload));
+        HIPCHK(h, hipStreamWaitEvent(h->stream, h->ev_upload, 0));
+        h->staged_pending = false;
+        if (values == nullptr) h->values_ptr = h->values.p;
+    }
     if (values == nullptr) {
         if (!h->values_ptr && S.nnz > 0) return set_err(h, UNO_KKT_ERR_STATE, "no device values to reuse");
     } else if (values_on_device) {
         h->values_ptr = values;
     } else {
-        // option pin_host_values: the caller's buffer is page-locked once (hipHostRegister) so every later
-        // upload is a direct DMA; it is unregistered when the pointer changes or the handle is destroyed
-        // (a registration is keyed by pointer AND length: the same address with another pattern size is a
-        // new buffer).  The caller keeps a registered buffer allocated until it passes another pointer, calls
-        // uno_kkt_analyze again or destroys the handle (include/uno_kkt.h).
-        if (h->pin_host && S.nnz > 0 && (values != h->pinned_ptr || h->pinned_bytes != (size_t)S.nnz * sizeof(double))) {
-            if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
-            h->pinned_bytes = (size_t)S.nnz * sizeof(double);
-            h->pinned_ptr = hipHostRegister(const_cast<double*>(values), h->pinned_bytes, hipHostRegisterDefault) ==
-                                    hipSuccess ? values : nullptr;
-            (void)hipGetLastError();
-        }
+        pin_host_buffer(h, values);
         if (S.nnz > 0)
             HIPCHK(h, hipMemcpyAsync(h->values.p, values, S.nnz * sizeof(double), hipMemcpyHostToDevice, h->stream));
         h->values_ptr = h->values.p;

@@ -3251,17 +3251,38 @@ __global__ void k_set_done(uint32_t* __restrict__ done, const int32_t* __restric
 }
 
 // Per-factorization map for the dataflow backward solve: rxpos[row slot] = xs index of the row's
-// solution value (pass 0: xpos[original id] of every pivot; pass 1: rows >= p of every front).
-__global__ __launch_bounds__(64) void k_xpos(SolveArgs A, DfArgs D, int32_t* __restrict__ xpos, int32_t* __restrict__ rxpos,
-                                             int pass) {
-    for (int t = blockIdx.x; t < D.nf; t += gridDim.x) {  // the walk's fronts
+// solution value (pass 0: xpos[original id] of every pivot; pass 1: rows >= p of every front).  One thread
+// per walk front, its rows in groups of 4 (the group's loads issued together): the fronts are small, and
+// one block per front left the launch dispatch-bound (2 x 15 us at C3).
+__global__ __launch_bounds__(256) void k_xpos(SolveArgs A, DfArgs D, int32_t* __restrict__ xpos, int32_t* __restrict__ rxpos,
+                                              int pass) {
+    for (int t = blockIdx.x * 256 + threadIdx.x; t < D.nf; t += gridDim.x * 256) {  // the walk's fronts
         const int f = D.order[t];
         const int m = A.fm[f], p = A.fp[f];
         const int64_t ro = A.rows_off[f];
+        const int32_t* fr = A.frow + ro;
         if (pass == 0) {
-            for (int i = threadIdx.x; i < p; i += 64) xpos[A.frow[ro + i]] = (int32_t)(D.xs_off[f] + i);
+            const int32_t x0 = (int32_t)D.xs_off[f];
+            int i = 0;
+            for (; i + 4 <= p; i += 4) {
+                const int32_t r0 = fr[i], r1 = fr[i + 1], r2 = fr[i + 2], r3 = fr[i + 3];
+                xpos[r0] = x0 + i;
+                xpos[r1] = x0 + i + 1;
+                xpos[r2] = x0 + i + 2;
+                xpos[r3] = x0 + i + 3;
+            }
+            for (; i < p; ++i) xpos[fr[i]] = x0 + i;
         } else {
-            for (int i = p + threadIdx.x; i < m; i += 64) rxpos[ro + i] = xpos[A.frow[ro + i]];
+            int i = p;
+            for (; i + 4 <= m; i += 4) {
+                const int32_t r0 = fr[i], r1 = fr[i + 1], r2 = fr[i + 2], r3 = fr[i + 3];
+                const int32_t x0 = xpos[r0], x1 = xpos[r1], x2 = xpos[r2], x3 = xpos[r3];
+                rxpos[ro + i] = x0;
+                rxpos[ro + i + 1] = x1;
+                rxpos[ro + i + 2] = x2;
+                rxpos[ro + i + 3] = x3;
+            }
+            for (; i < m; ++i) rxpos[ro + i] = xpos[fr[i]];
         }
     }
 }
@@ -4277,10 +4298,10 @@ hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* x
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
                        int64_t n_top, int64_t top_base, hipStream_t s) {
     if (D.nf <= 0) return hipSuccess;
-    const int g = std::min(D.nf, 8192);
-    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(64), 0, s, A, D, xpos, rxpos, 0);
+    const int g = (D.nf + 255) / 256;
+    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(256), 0, s, A, D, xpos, rxpos, 0);
     if (n_top > 0) hipLaunchKernelGGL(k_xpos_top, dim3(grid_for(n_top, 256)), dim3(256), 0, s, top_orig, n_top, top_base, xpos);
-    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(64), 0, s, A, D, xpos, rxpos, 1);
+    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(256), 0, s, A, D, xpos, rxpos, 1);
     return hipGetLastError();
 }
 

@@ -81,6 +81,7 @@ def load_library():
     lib.uno_kkt_analyze.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, _i64p, _i64p]
     lib.uno_kkt_factorize.argtypes = [vp, ctypes.c_void_p, ctypes.c_int]
     lib.uno_kkt_factorize_update.argtypes = [vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]
+    lib.uno_kkt_stage_values.argtypes = [vp, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64]
     lib.uno_kkt_set_values.argtypes = [vp, _i64p, _f64p, ctypes.c_int64]
     lib.uno_kkt_fill_values.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_double]
     lib.uno_kkt_inertia.argtypes = [vp, _i64p, _i64p, _i64p]
@@ -196,6 +197,13 @@ class HipKKT:
         # referenced too, as an asynchronous copy from it may still be in flight
         self._v_upd = v
         self._check(self.lib.uno_kkt_factorize_update(self.h, v.ctypes.data_as(ctypes.c_void_p), int(first), int(count)))
+
+    def stage_values(self, values, first, count):
+        """Asynchronous upload of values[first, first+count) (host array, COO order); the next factorize()
+        without arguments factors the staged values (uno_kkt_stage_values)."""
+        v, _ = _f64(values)
+        self._v_stage = v  # the copy reads it asynchronously: keep it referenced
+        self._check(self.lib.uno_kkt_stage_values(self.h, v.ctypes.data_as(ctypes.c_void_p), int(first), int(count)))
 
     def fill_values(self, first, count, value):
         self._check(self.lib.uno_kkt_fill_values(self.h, int(first), int(count), float(value)))
