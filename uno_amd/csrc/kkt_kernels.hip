@@ -3509,6 +3509,10 @@ __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __
 #pragma unroll
     for (int c = 0; c < kAppNB; ++c) a[c] = (lane < nb && c <= lane) ? row[c] : 0.0;
     int nbt = nb;
+    // pivot c's d and block-local column maximum stay in lane c's registers until the loop ends: a global
+    // store per step would make every step's barrier wait for its completion.  One wave: its LDS operations
+    // complete in issue order, so the column broadcast needs no workgroup barrier either.
+    double dmine = 0.0, gmine = 0.0;
 #pragma unroll
     for (int c = 0; c < kAppNB; ++c) {
         if (c >= nbt) continue;  // uniform (no break: the loop stays unrolled, a[] in registers)
@@ -3516,13 +3520,18 @@ __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __
         const double g = wave_max_abs((lane > c && lane < nb) ? fabs(a[c]) : 0.0);
         const double aak = fabs(akk);
         if (!(aak > thres) || A.u * g > aak) { nbt = c; continue; }  // uniform
-        if (lane == 0) { sl->d[c] = akk; sl->cmax[c] = as_bits(g); }
+        dmine = lane == c ? akk : dmine;
+        gmine = lane == c ? g : gmine;
         const double l = lane > c ? a[c] * (1.0 / akk) : 0.0;
         colc[lane] = a[c];  // W(k + lane, c)
-        __syncthreads();
+        __asm__ volatile("" ::: "memory");
 #pragma unroll
         for (int j = c + 1; j < kAppNB; ++j) a[j] -= l * colc[j];
-        __syncthreads();
+        __asm__ volatile("" ::: "memory");
+    }
+    if (lane < nbt) {
+        sl->d[lane] = dmine;
+        sl->cmax[lane] = as_bits(gmine);
     }
     if (lane < nbt) {
         double* pr = app_panel(A, f, m) + (int64_t)lane * kAppNB;
