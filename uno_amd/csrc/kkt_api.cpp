@@ -208,6 +208,8 @@ struct uno_kkt {
     int df_consec_aborts = 0;      // consecutive aborted dataflow solves (kMaxDfAborts turns the walk off)
     int debug_abort_solves = 0;    // option debug_abort_solves: the next k dataflow solves start with the abort flag set (tests)
     DBuf<int32_t> df_order, df_desc, df_xpos, df_rxpos;
+    DBuf<int32_t> df_rowx;                // per front row: xs slot of a walk front's pivot position, -2: its
+                                          // contribution row, -1: not in the walk (k_xpos)
     DBuf<int32_t> rg_desc, ov_desc;  // register kernels: the walk split into p <= 32, m <= 72 fronts and the others
     int32_t rg_nf = 0, ov_nf = 0, ov_grid = 0;
     DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
@@ -380,6 +382,7 @@ DfArgs dataflow_args(uno_kkt_t h) {
     D.order = h->df_order.p; D.desc = h->df_desc.p; D.nf = h->df_nwalk; D.parent = h->fparent.p; D.cnt = h->df_cnt.p;
     D.done = h->df_done.p; D.epoch = h->df_epoch; D.cvx = h->df_cvx.p; D.cvx_off = h->df_cvx_off.p;
     D.ch_cvx_off = h->df_ch_cvx_off.p; D.xs = h->df_xs.p; D.xs_off = h->df_xs_off.p; D.rxpos = h->df_rxpos.p;
+    D.rowx = h->df_rowx.p; D.rows_total = (int64_t)h->S.rows.size();
     D.abort_flag = h->df_abort.p;
     D.win = h->df_win;
     D.piv_off = h->df_piv_off;
@@ -1025,6 +1028,14 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     if ((e = h->df_xs.alloc(std::max<int64_t>(tx, 16))) != hipSuccess) return e;
     if ((e = h->df_xpos.alloc(std::max<int64_t>(S.n, 1))) != hipSuccess) return e;
     if ((e = h->df_rxpos.alloc(std::max<size_t>(S.rows.size(), 1))) != hipSuccess) return e;
+    {
+        std::vector<int32_t> rowx(std::max<size_t>(S.rows.size(), 1), -1);
+        for (int32_t f : walk) {
+            const int64_t ro = S.f_rows_off[f];
+            for (int i = 0; i < S.f_m[f]; ++i) rowx[ro + i] = i < S.f_p[f] ? (int32_t)(xs[f] + i) : -2;
+        }
+        if ((e = h->df_rowx.upload(rowx, s)) != hipSuccess) return e;
+    }
     if ((e = h->df_cnt.alloc(S.nf)) != hipSuccess) return e;
     if ((e = h->df_done.alloc(S.nf)) != hipSuccess) return e;
     if (!h->df_abort.p && (e = h->df_abort.alloc(1)) != hipSuccess) return e;

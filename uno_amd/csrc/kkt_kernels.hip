@@ -2386,20 +2386,40 @@ __device__ __forceinline__ double bwd_compute_win(const double* __restrict__ L, 
         const double* pk = P + (pcol(m, mine ? lane : c0) - base);  // pk[i] = L(i, lane), i >= lane
         double s0 = 0.0, s1 = 0.0;
         int i = p;
+        // four pairs' operands read before their products (one LDS wait per 8 rows instead of per 2); the
+        // products accumulate in the same order as the pairwise loop below (s0: rows p, p+2, ...; s1: odd)
+        for (; i + 7 < m; i += 8) {
+            double a[8], b[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) { a[u] = pk[i + u]; b[u] = x[i + u]; }
+#pragma unroll
+            for (int u = 0; u < 8; u += 2) {
+                s0 += a[u] * b[u];
+                s1 += a[u + 1] * b[u + 1];
+            }
+        }
         for (; i + 1 < m; i += 2) {
             s0 += pk[i] * x[i];
             s1 += pk[i + 1] * x[i + 1];
         }
         if (i < m) s0 += pk[i] * x[i];
         if (live && mine) xj -= s0 + s1;
-        for (int k = p - 1; k >= c0; --k) {
-            const double l = pk[k];
+        auto step = [&](int k, double l) {
             const int kind = __builtin_amdgcn_readlane(mypiv, k);
             const double xk = kind != PIV_NULL ? readlane_d(xj, k) : 0.0;
             const int skip = kind == PIV_2X2_B ? k - 1 : -1;
             const double t = xj - l * xk;
             xj = (live && mine && lane < k && lane != skip) ? t : xj;
+        };
+        int k = p - 1;
+        for (; k - 3 >= c0; k -= 4) {  // four steps' operands read first (the chain runs through xj only)
+            double l4[4];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) l4[u] = pk[k - u];
+#pragma unroll
+            for (int u = 0; u < 4; ++u) step(k - u, l4[u]);
         }
+        for (; k >= c0; --k) step(k, pk[k]);
         if (c0 == 0) break;
         c1 = c0;
         c0 = bwd_chunk_begin(m, p, c1, win);
@@ -3251,38 +3271,18 @@ __global__ void k_set_done(uint32_t* __restrict__ done, const int32_t* __restric
 }
 
 // Per-factorization map for the dataflow backward solve: rxpos[row slot] = xs index of the row's
-// solution value (pass 0: xpos[original id] of every pivot; pass 1: rows >= p of every front).  One thread
-// per walk front, its rows in groups of 4 (the group's loads issued together): the fronts are small, and
-// one block per front left the launch dispatch-bound (2 x 15 us at C3).
-__global__ __launch_bounds__(256) void k_xpos(SolveArgs A, DfArgs D, int32_t* __restrict__ xpos, int32_t* __restrict__ rxpos,
-                                              int pass) {
-    for (int t = blockIdx.x * 256 + threadIdx.x; t < D.nf; t += gridDim.x * 256) {  // the walk's fronts
-        const int f = D.order[t];
-        const int m = A.fm[f], p = A.fp[f];
-        const int64_t ro = A.rows_off[f];
-        const int32_t* fr = A.frow + ro;
+// solution value (pass 0: xpos[original id] of every pivot; pass 1: rows >= p of every front).  Flat over
+// the front rows (coalesced): rowx (per analysis) holds each walk front's pivot-position xs slot, or -2 for its
+// contribution rows; frow (per factorization) the row now at that position.  One block per front left both
+// passes dispatch-bound (2 x 15 us at C3), one thread per front gather-bound (2 x 25 us).
+__global__ void k_xpos(DfArgs D, const int32_t* __restrict__ frow, int32_t* __restrict__ xpos,
+                       int32_t* __restrict__ rxpos, int pass) {
+    for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < D.rows_total; t += (int64_t)gridDim.x * blockDim.x) {
+        const int32_t v = D.rowx[t];
         if (pass == 0) {
-            const int32_t x0 = (int32_t)D.xs_off[f];
-            int i = 0;
-            for (; i + 4 <= p; i += 4) {
-                const int32_t r0 = fr[i], r1 = fr[i + 1], r2 = fr[i + 2], r3 = fr[i + 3];
-                xpos[r0] = x0 + i;
-                xpos[r1] = x0 + i + 1;
-                xpos[r2] = x0 + i + 2;
-                xpos[r3] = x0 + i + 3;
-            }
-            for (; i < p; ++i) xpos[fr[i]] = x0 + i;
-        } else {
-            int i = p;
-            for (; i + 4 <= m; i += 4) {
-                const int32_t r0 = fr[i], r1 = fr[i + 1], r2 = fr[i + 2], r3 = fr[i + 3];
-                const int32_t x0 = xpos[r0], x1 = xpos[r1], x2 = xpos[r2], x3 = xpos[r3];
-                rxpos[ro + i] = x0;
-                rxpos[ro + i + 1] = x1;
-                rxpos[ro + i + 2] = x2;
-                rxpos[ro + i + 3] = x3;
-            }
-            for (; i < m; ++i) rxpos[ro + i] = xpos[fr[i]];
+            if (v >= 0) xpos[frow[t]] = v;
+        } else if (v == -2) {
+            rxpos[t] = xpos[frow[t]];
         }
     }
 }
@@ -4307,10 +4307,10 @@ hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* x
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
                        int64_t n_top, int64_t top_base, hipStream_t s) {
     if (D.nf <= 0) return hipSuccess;
-    const int g = (D.nf + 255) / 256;
-    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(256), 0, s, A, D, xpos, rxpos, 0);
+    const dim3 g(grid_for(D.rows_total, 256));
+    hipLaunchKernelGGL(k_xpos, g, dim3(256), 0, s, D, A.frow, xpos, rxpos, 0);
     if (n_top > 0) hipLaunchKernelGGL(k_xpos_top, dim3(grid_for(n_top, 256)), dim3(256), 0, s, top_orig, n_top, top_base, xpos);
-    hipLaunchKernelGGL(k_xpos, dim3(g), dim3(256), 0, s, A, D, xpos, rxpos, 1);
+    hipLaunchKernelGGL(k_xpos, g, dim3(256), 0, s, D, A.frow, xpos, rxpos, 1);
     return hipGetLastError();
 }
 

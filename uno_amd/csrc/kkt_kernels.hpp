@@ -117,6 +117,8 @@ struct DfArgs {
     double* xs;                 // solution vector in elimination order: each front's pivots in a 128-byte-aligned slot
     const int64_t* xs_off;      // per front
     const int32_t* rxpos;       // per front row (layout of frow): xs index of the rows >= p
+    const int32_t* rowx;        // per front row: xs slot of a walk front's pivot position, -2 its contribution rows, -1
+    int64_t rows_total;         // length of rowx
     uint32_t* abort_flag;       // set when a wait exceeded its limit (result invalid, host falls back)
     int32_t win;                // LDS panel window (doubles, even, >= the longest column); rows follow it
     int32_t piv_off;            // LDS offset (doubles) of the 64 pivot-kind words, after the rows
