@@ -221,6 +221,7 @@ struct uno_kkt {
     // "dataflow_factor" (default 1)
     int concurrent_classes = 1;  // option "concurrent_classes"
     int early_xpos = 1;          // option "early_xpos": the dataflow solve's row maps queued with the factorization
+    bool xpos_by_factor = false; // the last factorization wrote xpos itself (FactorArgs::xpos)
     hipEvent_t ev_counters = nullptr;  // after the counters' read-back of the last enqueued factorization
     hipEvent_t ev_wait = nullptr;      // host_wait_stream
     int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
@@ -1279,7 +1280,7 @@ hipError_t enqueue_xpos(uno_kkt_t h) {
     A.L_off = h->L_off.p; A.L = h->L.p; A.w = h->w.p; A.cvec = h->cvec.p; A.ch_cm = h->ch_cm.p;
     A.ch_relmap_off = h->ch_relmap_off.p;
     const DfArgs Df = dataflow_args(h);
-    hipError_t e = launch_xpos(A, Df, h->df_xpos.p, h->df_rxpos.p, nullptr, 0, h->df_top_base, h->stream);
+    hipError_t e = launch_xpos(A, Df, h->df_xpos.p, h->df_rxpos.p, nullptr, 0, h->df_top_base, h->stream, !h->xpos_by_factor);
     if (e == hipSuccess) h->df_rx_valid = true;
     return e;
 }
@@ -1359,6 +1360,10 @@ int enqueue_factorization(uno_kkt_t h) {
         HIPCHK(h, launch_front_scale(h->rows.p, h->scale.p, h->fscale.p, (int64_t)S.rows.size(), s));
     FactorArgs A;
     A.fscale = h->front_scale ? h->fscale.p : nullptr;
+    // one GPU with the dataflow solve: the factor write-outs also fill xpos (k_xpos pass 0)
+    h->xpos_by_factor = h->world == 1 && h->df_enabled && h->df_grid > 0 && h->early_xpos && h->df_xpos.p && h->df_xs_off.p;
+    A.xpos = h->xpos_by_factor ? h->df_xpos.p : nullptr;
+    A.xs_off = h->xpos_by_factor ? h->df_xs_off.p : nullptr;
     A.fm = h->fm.p; A.fp = h->fp.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p;
     A.ent_off = h->ent_off.p; A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.scale = h->scale.p;
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;

@@ -1449,6 +1449,8 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         A.frow[A.rows_off[f] + i] = lrow[i];
         A.fpos[A.rows_off[f] + lorig[i]] = i;  // analysis-order local row -> pivoted position
         if (i < p) A.piv[A.rows_off[f] + i] = piv[i];
+        // one GPU, dataflow solve: the pivot's solution slot (k_xpos pass 0, written here instead)
+        if (i < p && A.xpos) A.xpos[lrow[i]] = (int32_t)(A.xs_off[f] + i);
     }
     if (sub) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
     // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
@@ -3844,6 +3846,8 @@ __global__ __launch_bounds__(kThreads) void k_big_finish(FactorArgs A, const int
     for (int i = tid; i < m; i += kThreads) lorig[i] = A.fpos[ro + i];
     __syncthreads();
     for (int i = tid; i < m; i += kThreads) A.fpos[ro + lorig[i]] = i;
+    if (A.xpos)  // see factor_front's row-id write-out
+        for (int i = tid; i < p; i += kThreads) A.xpos[A.frow[ro + i]] = (int32_t)(A.xs_off[f] + i);
     if (tid == 0) {
         const BigFrontState S = A.big[f];
         A.fstat[f] = (int32_t)((S.nstuck > 0xffff ? 0xffff : S.nstuck) | ((S.nrel > 0x7fff ? 0x7fff : S.nrel) << 16));
@@ -4305,10 +4309,10 @@ hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* x
 }
 
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
-                       int64_t n_top, int64_t top_base, hipStream_t s) {
+                       int64_t n_top, int64_t top_base, hipStream_t s, bool pass0) {
     if (D.nf <= 0) return hipSuccess;
     const dim3 g(grid_for(D.rows_total, 256));
-    hipLaunchKernelGGL(k_xpos, g, dim3(256), 0, s, D, A.frow, xpos, rxpos, 0);
+    if (pass0) hipLaunchKernelGGL(k_xpos, g, dim3(256), 0, s, D, A.frow, xpos, rxpos, 0);
     if (n_top > 0) hipLaunchKernelGGL(k_xpos_top, dim3(grid_for(n_top, 256)), dim3(256), 0, s, top_orig, n_top, top_base, xpos);
     hipLaunchKernelGGL(k_xpos, g, dim3(256), 0, s, D, A.frow, xpos, rxpos, 1);
     return hipGetLastError();

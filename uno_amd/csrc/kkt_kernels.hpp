@@ -79,6 +79,8 @@ struct FactorArgs {
     uint32_t* df_ticket;        // block start order (cumulative: (epoch - 1) * df_nf at launch)
     uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
     BigFrontState* big;         // per front: state of the blocked large-front factorization (m > kMaxLdsFront)
+    int32_t* xpos = nullptr;        // one GPU, dataflow solve: xpos[row] = xs slot of each pivot (k_xpos pass 0)
+    const int64_t* xs_off = nullptr;  // per front: its xs slot (DfArgs::xs_off)
 };
 
 struct SolveArgs {
@@ -279,7 +281,8 @@ hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int ld
 // runs: the walk is the rank's own fronts, and the top rows (top_orig, eliminated on rank 0) get the
 // slots top_base + t of xs, where the broadcast top solution is copied before the backward launch
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
-                       int64_t n_top, int64_t top_base, hipStream_t s);
+                       int64_t n_top, int64_t top_base, hipStream_t s,
+                       bool pass0 = true);
 // xs[xpos[i]] = scale_i b_i  /  x_i = scale_i xs[xpos[i]]; rows i = list[0 .. n) (list == nullptr: 0 .. n-1)
 hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s,
                         const int32_t* list = nullptr);
