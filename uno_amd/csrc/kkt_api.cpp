@@ -1454,7 +1454,8 @@ int enqueue_factorization(uno_kkt_t h) {
         A.df_abort = h->df_abort.p;
         A.df_ticket = h->dff_ticket.p;
         HIPCHK(h, launch_factor_df(A, h->dff_mmax, s));
-        HIPCHK(h, hipMemcpyAsync(h->h_counters + 11, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        // one GPU: k_count writes the abort word to the host block itself
+        if (h->world > 1) HIPCHK(h, hipMemcpyAsync(h->h_counters + 11, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
     }
     if (h->world > 1) {
         // subtree roots' contribution blocks -> rank 0 (same arena offsets on every rank)
@@ -1471,14 +1472,19 @@ int enqueue_factorization(uno_kkt_t h) {
             }
         }
     }
-    HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits_p, s));
+    if (h->world == 1) {  // counters and the dataflow abort word straight into the page-locked host block
+        HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits_p, s,
+                               dff ? h->df_abort.p : nullptr, h->h_counters));
+    } else {
+        HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits_p, s));
+    }
     if (h->world > 1) {
         // counters[7] keeps this rank's delayed-column count; 0..6 are summed over the ranks
         HIPCHK(h, hipMemcpyAsync(h->counters.p + 7, h->counters.p + 6, sizeof(unsigned long long), hipMemcpyDeviceToDevice, s));
         HIPCHK(h, h->comm->allreduce(h->counters.p, 7, RedOp::SumU64, s));
     }
     // counters and minbits in one copy (h_counters[8] is the min pivot bits)
-    HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
+    if (h->world > 1) HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
     HIPCHK(h, hipEventRecord(h->ev_counters, s));  // sync_and_verify waits for this, not for the xpos below
     h->factor_enqueued = true;
     h->df_rx_valid = false;  // pivoting may have permuted rows

@@ -4080,10 +4080,13 @@ hipError_t launch_factor(const FactorArgs& A, const int32_t* fronts, int count, 
     return hipGetLastError();
 }
 
+// host_out (one GPU): the last block to finish also writes counters [0..8] and the dataflow abort word (slot
+// 11) straight into the page-locked host block -- the two device-to-host copies that followed are gone
 __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restrict__ fcnt,
                                                const int32_t* __restrict__ fstat, const double* __restrict__ fmin,
                                                int64_t nf, unsigned long long* __restrict__ counters,
-                                               unsigned long long* __restrict__ minbits) {
+                                               unsigned long long* __restrict__ minbits, const uint32_t* __restrict__ abort_word,
+                                               unsigned long long* __restrict__ host_out) {
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long mn = ~0ull;
     for (int64_t f = blockIdx.x * 256 + threadIdx.x; f < nf; f += (int64_t)gridDim.x * 256) {
@@ -4117,13 +4120,25 @@ __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restr
         for (int w = 1; w < 4; ++w) v = rmin[w] < v ? rmin[w] : v;
         atomicMin(minbits, v);
     }
+    if (host_out == nullptr) return;
+    __shared__ int last;
+    __threadfence();
+    __syncthreads();
+    if (threadIdx.x == 0) last = atomicAdd(reinterpret_cast<unsigned int*>(counters + 10), 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!last) return;
+    __threadfence();
+    if (threadIdx.x < 9)
+        host_out[threadIdx.x] = __hip_atomic_load(counters + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 11) host_out[11] = abort_word ? (unsigned long long)__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
 }
 
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
-                        unsigned long long* counters, unsigned long long* minbits, hipStream_t s) {
-    if (nf <= 0) return hipSuccess;
-    const int blocks = (int)std::min<int64_t>(64, (nf + 255) / 256);
-    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, fmin, nf, counters, minbits);
+                        unsigned long long* counters, unsigned long long* minbits, hipStream_t s, const uint32_t* abort_word,
+                        unsigned long long* host_out) {
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(64, (nf + 255) / 256));
+    if (nf <= 0 && host_out == nullptr) return hipSuccess;
+    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, fmin, nf, counters, minbits, abort_word, host_out);
     return hipGetLastError();
 }
 

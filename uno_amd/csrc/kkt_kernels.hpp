@@ -246,9 +246,10 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
                              hipStream_t s);
 // counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
-                        unsigned long long* counters, unsigned long long* minbits, hipStream_t s);
+                        unsigned long long* counters, unsigned long long* minbits, hipStream_t s,
+                        const uint32_t* abort_word = nullptr, unsigned long long* host_out = nullptr);
 // the factorization's device counter block: [0..7] pivot counters, [8] min pivot bits, [9] ||A_pre||_inf bits
-constexpr int kCounterSlots = 10;
+constexpr int kCounterSlots = 11;  // [10]: k_count's block ticket (host_out)
 hipError_t launch_reset_counters(unsigned long long* counters, hipStream_t s);
 // fscale[t] = scale[rows[t]] for every front row t (one gather after the equilibration: the front assembly then
 // loads its rows' scalings in the same round trip as the row ids instead of after them)
