@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = [
     "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info", "uno_kkt_rhs_setup",
     "uno_kkt_assemble_rhs", "uno_kkt_assemble_direction", "uno_kkt_symv", "uno_kkt_quadratic_product",
     "uno_kkt_barrier_setup", "uno_kkt_barrier_count", "uno_kkt_assemble_barrier", "uno_kkt_attach_host",
+    "uno_kkt_stage_values",
 ]
 
 
