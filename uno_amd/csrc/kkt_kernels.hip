@@ -17,6 +17,7 @@
 #include <cstdlib>
 #include <cstdint>
 #include <type_traits>
+#include <utility>
 
 #include "kkt_kernels.hpp"
 
@@ -742,6 +743,18 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x)
 }
 // non-negative doubles compare like their bit patterns
 __device__ __forceinline__ double wave_max_abs(double v) { return as_double(wave_max_u64(as_bits(v))); }
+// an upper bound of wave_max_abs within 2^-20 relative: the maximum of the high words, low word all ones (one
+// 32-bit DPP chain instead of the 64-bit compare-and-select one)
+__device__ __forceinline__ double wave_max_abs_ub(double v) {
+    unsigned x = (unsigned)(as_bits(v) >> 32);
+    x = max(x, (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xf, 0xf, false));
+    x = max(x, (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xf, 0xf, false));
+    x = max(x, (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xf, 0xf, false));
+    x = max(x, (unsigned)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xf, 0xf, false));
+    const unsigned h = max(max((unsigned)__builtin_amdgcn_readlane((int)x, 0), (unsigned)__builtin_amdgcn_readlane((int)x, 16)),
+                           max((unsigned)__builtin_amdgcn_readlane((int)x, 32), (unsigned)__builtin_amdgcn_readlane((int)x, 48)));
+    return h >= 0x7ff00000u ? INFINITY : as_double(((unsigned long long)h << 32) | 0xffffffffull);  // inf / NaN: inf
+}
 
 template <class S> constexpr bool kFullStore = std::is_same<S, FullStore>::value;
 
@@ -3468,9 +3481,8 @@ __global__ __launch_bounds__(kThreads) void k_big_update(FactorArgs A, const int
 // One step takes the next kAppNB columns of every unfinished large front in three launches, so the trailing
 // matrix is read and written once per kAppNB pivots (one rank-kAppNB MFMA update) instead of once per
 // register panel of 8 or 16:
-//   k_app_diag   one wave per front: the diagonal block right-looking in registers (lane = row), each
-//                column's quick Duff-Reid 1x1 test over the block's rows; the first failure ends the block
-//                (nbt columns pass).  W (un-normalised columns) into the step's panel, pivots into AppSlot.
+//   k_app_diag   one wave per front: the diagonal block right-looking in registers (lane = row), each column's quick Duff-Reid 1x1 test, else the 2x2 test with the next column,
+//                over the block's rows; the first failure ends the block (nbt columns pass).  W (un-normalised columns) into the step's panel, pivots into AppSlot.
 //   k_app_rows   the rows below, one per lane: W(i, c) = A(i, c) - sum_{q < c} L(i, q) W(c, q), L = W / d
 //                (k_big_panel_reg's products, pivots ascending), into the panel; per-column max |W(i, c)|
 //                by atomic max of the bits.  The last block to arrive applies the complete quick test
@@ -3491,8 +3503,20 @@ __device__ __forceinline__ AppSlot* app_slot(const FactorArgs& A, int f, int m) 
     return reinterpret_cast<AppSlot*>(app_panel(A, f, m) + (int64_t)m * kAppNB);
 }
 
+template <class F, int... I>
+__device__ __forceinline__ void each_index(F& f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+
+// One wave (lane = row).  Pivot c's d, block-local column maximum, off-diagonal and kind stay in lane c's
+// registers until the loop ends: a global store per step would make every step's barrier wait for its
+// completion.  One wave: its LDS operations complete in issue order, so the column broadcast needs no barrier.
+// The 64 steps are expanded at compile time (each_index): a[] indices stay constants, i.e. registers (the plain
+// unrolled loop with the 2x2 branch passes the full-unroll limit, and the rolled one indexes a[] from scratch).
+// The tests run on upper bounds of the column maxima (wave_max_abs_ub), recorded as such: conservative by 2^-20
+// at most, so every accepted pivot passes the exact test, and a borderline one is left to k_app_exact's exact rule.
 __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __restrict__ fronts) {
-    __shared__ double colc[kAppNB];
+    __shared__ double colc[kAppNB], colc1[kAppNB];
     const int lane = threadIdx.x;
     const int f = fronts[blockIdx.x];
     const int m = A.fm[f], p = A.fp[f];
@@ -3511,31 +3535,65 @@ __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __
 #pragma unroll
     for (int c = 0; c < kAppNB; ++c) a[c] = (lane < nb && c <= lane) ? row[c] : 0.0;
     int nbt = nb;
-    // pivot c's d and block-local column maximum stay in lane c's registers until the loop ends: a global
-    // store per step would make every step's barrier wait for its completion.  One wave: its LDS operations
-    // complete in issue order, so the column broadcast needs no workgroup barrier either.
-    double dmine = 0.0, gmine = 0.0;
-#pragma unroll
-    for (int c = 0; c < kAppNB; ++c) {
-        if (c >= nbt) continue;  // uniform (no break: the loop stays unrolled, a[] in registers)
-        const double akk = __shfl(a[c], c);
-        const double g = wave_max_abs((lane > c && lane < nb) ? fabs(a[c]) : 0.0);
+    double dmine = 0.0, gmine = 0.0, omine = 0.0;
+    int kmine = PIV_1X1;
+    bool second = false;  // column c is the second of an accepted 2x2 pair (uniform)
+    auto step = [&](auto cc) {
+        constexpr int c = decltype(cc)::value;
+        if (c >= nbt) return;  // uniform
+        if (second) { second = false; return; }
+        const double akk = readlane_d(a[c], c);
+        const double g = wave_max_abs_ub((lane > c && lane < nb) ? fabs(a[c]) : 0.0);
         const double aak = fabs(akk);
-        if (!(aak > thres) || A.u * g > aak) { nbt = c; continue; }  // uniform
-        dmine = lane == c ? akk : dmine;
-        gmine = lane == c ? g : gmine;
-        const double l = lane > c ? a[c] * (1.0 / akk) : 0.0;
-        colc[lane] = a[c];  // W(k + lane, c)
-        __asm__ volatile("" ::: "memory");
+        if (aak > thres && !(A.u * g > aak)) {  // 1x1 (uniform)
+            dmine = lane == c ? akk : dmine;
+            gmine = lane == c ? g : gmine;
+            const double l = lane > c ? a[c] * (1.0 / akk) : 0.0;
+            colc[lane] = a[c];  // W(k + lane, c)
+            __asm__ volatile("" ::: "memory");
 #pragma unroll
-        for (int j = c + 1; j < kAppNB; ++j) a[j] -= l * colc[j];
-        __asm__ volatile("" ::: "memory");
-    }
+            for (int j = c + 1; j < kAppNB; ++j) a[j] -= l * colc[j];
+            __asm__ volatile("" ::: "memory");
+            return;
+        }
+        // 2x2 with the next column, no interchange: Duff-Reid's 2x2 test (oracle test_pivot's inequalities) on the
+        // block's rows below the pair now, on every row below it a posteriori (k_app_rows).  A valid threshold
+        // pivot -- not always the partner MUMPS would pick (the argmax row): large fronts are checked by inertia
+        // and residual, not bit for bit.
+        constexpr int cn = c + 1 < kAppNB ? c + 1 : c;
+        if (c + 1 < nb) {  // uniform
+            const double b = readlane_d(a[c], cn), dd = readlane_d(a[cn], cn);
+            const double gc = wave_max_abs_ub((lane > c + 1 && lane < nb) ? fabs(a[c]) : 0.0);
+            const double gr = wave_max_abs_ub((lane > c + 1 && lane < nb) ? fabs(a[cn]) : 0.0);
+            const double det = akk * dd - b * b;
+            const double lim = fabs(det) / A.u;
+            if (det != 0.0 && fmax(aak, fabs(b)) > thres && fabs(dd) > 0.0 && fabs(dd) * gc + fabs(b) * gr <= lim &&
+                fabs(b) * gc + aak * gr <= lim) {
+                dmine = lane == c ? akk : (lane == c + 1 ? dd : dmine);
+                gmine = lane == c ? gc : (lane == c + 1 ? gr : gmine);
+                omine = lane == c || lane == c + 1 ? b : omine;
+                kmine = lane == c ? PIV_2X2_A : (lane == c + 1 ? PIV_2X2_B : kmine);
+                const double inv = 1.0 / det;
+                const double l0 = lane > c + 1 ? (dd * a[c] - b * a[cn]) * inv : 0.0;
+                const double l1 = lane > c + 1 ? (akk * a[cn] - b * a[c]) * inv : 0.0;
+                colc[lane] = a[c];
+                colc1[lane] = a[cn];
+                __asm__ volatile("" ::: "memory");
+#pragma unroll
+                for (int j = c + 2; j < kAppNB; ++j) a[j] -= l0 * colc[j] + l1 * colc1[j];
+                __asm__ volatile("" ::: "memory");
+                second = true;
+                return;
+            }
+        }
+        nbt = c;  // uniform
+    };
+    each_index(step, std::make_integer_sequence<int, kAppNB>{});
     if (lane < nbt) {
         sl->d[lane] = dmine;
         sl->cmax[lane] = as_bits(gmine);
-    }
-    if (lane < nbt) {
+        sl->offd[lane] = omine;
+        sl->kind[lane] = (int8_t)kmine;
         double* pr = app_panel(A, f, m) + (int64_t)lane * kAppNB;
 #pragma unroll
         for (int c = 0; c < kAppNB; ++c)
@@ -3545,6 +3603,27 @@ __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __
         sl->k0 = k; sl->nbt = nbt; sl->nb = nb; sl->nacc = 0; sl->arrive = 0u;
         if (nbt == 0) Sg->exact = 1;  // the first column fails already within the block
         Sg->k0 = Sg->k1;              // nothing pending for k_big_update unless the register panel runs
+    }
+}
+
+// L(i, c) = cself[c] W(i, c) + coth[c] W(i, partner(c)) for the accepted pivot columns of an a-posteriori step:
+// 1x1: 1 / d; 2x2 pair (a, b; b, e) = the columns (c, c + 1): L(i, c) = (e W_c - b W_c+1) / det, L(i, c + 1) =
+// (a W_c+1 - b W_c) / det (the oracle's elim_2x2 with the inverse precomputed)
+__device__ __forceinline__ void app_coefs(const AppSlot* sl, int c, int nbt, double& cself, double& coth, int& partner) {
+    cself = 0.0;
+    coth = 0.0;
+    partner = c;
+    if (c >= nbt) return;
+    const int kind = sl->kind[c];
+    if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+        const int c0 = kind == PIV_2X2_A ? c : c - 1;
+        const double a = sl->d[c0], e = sl->d[c0 + 1], b = sl->offd[c0];
+        const double inv = 1.0 / (a * e - b * b);
+        cself = (kind == PIV_2X2_A ? e : a) * inv;
+        coth = -b * inv;
+        partner = kind == PIV_2X2_A ? c + 1 : c - 1;
+    } else {
+        cself = 1.0 / sl->d[c];
     }
 }
 
@@ -3563,7 +3642,8 @@ __device__ __forceinline__ double quad_bcast(double v, int s) {
 __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* __restrict__ fronts) {
     __shared__ __attribute__((aligned(16))) double WdS[kAppNB][4][kAppNB / 4];  // W(k0 + 4jj + q, c) at [c][q][jj]
     __shared__ double amax[kAppNB][kAppNB + 1];                              // |W| of the block's rows, [col][row]
-    __shared__ double dinv[kAppNB];
+    __shared__ double cself[kAppNB], coth[kAppNB];                           // app_coefs
+    __shared__ int kindS[kAppNB];
     __shared__ int last;
     const int tid = threadIdx.x, q = tid & 3, rl = tid >> 2;
     const int lane = tid & 63;
@@ -3574,11 +3654,17 @@ __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* _
     if (nbt == 0) return;  // no step for this front (done, or the register panel's exact search is next)
     const int k0 = sl->k0;
     double* P = app_panel(A, f, m);
+    // the pair's second row (W(c + 1, c) = its off-diagonal) is not an update operand of the pair's columns
     for (int t = tid; t < kAppNB * kAppNB; t += 256) {
         const int j = t >> 6, c = t & 63;
-        WdS[c][j & 3][j >> 2] = (c < j && j < nbt) ? P[(int64_t)j * kAppNB + c] : 0.0;
+        const bool pairrow = c < nbt && j == c + 1 && sl->kind[c] == PIV_2X2_A;
+        WdS[c][j & 3][j >> 2] = (c < j && j < nbt && !pairrow) ? P[(int64_t)j * kAppNB + c] : 0.0;
     }
-    if (tid < kAppNB) dinv[tid] = tid < nbt ? 1.0 / sl->d[tid] : 0.0;
+    if (tid < kAppNB) {
+        int pt;
+        app_coefs(sl, tid, nbt, cself[tid], coth[tid], pt);
+        kindS[tid] = tid < nbt ? (int)sl->kind[tid] : PIV_1X1;
+    }
     __syncthreads();
     const FullStore st{A.gscratch + A.gscratch_off[f], m};
     const int i = k0 + nbt + (int)blockIdx.x * 64 + rl;
@@ -3589,7 +3675,18 @@ __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* _
     for (int jj = 0; jj < kAppNB / 4; ++jj) w[jj] = (valid && 4 * jj + q < nbt) ? row[4 * jj + q] : 0.0;
 #pragma unroll
     for (int c = 0; c < kAppNB; ++c) {
-        const double l = quad_bcast(w[c >> 2] * dinv[c], c & 3);  // 0 from column nbt on
+        const int kc = kindS[c];  // uniform
+        if (kc == PIV_2X2_B) continue;  // applied with its first column
+        if (c + 1 < kAppNB && kc == PIV_2X2_A) {
+            const double wc = quad_bcast(w[c >> 2], c & 3), wr = quad_bcast(w[(c + 1) >> 2], (c + 1) & 3);
+            const double l0 = cself[c] * wc + coth[c] * wr, l1 = cself[c + 1] * wr + coth[c + 1] * wc;
+            const double* wd0 = &WdS[c][q][0];
+            const double* wd1 = &WdS[c + 1][q][0];
+#pragma unroll
+            for (int jj = c >> 2; jj < kAppNB / 4; ++jj) w[jj] -= l0 * wd0[jj] + l1 * wd1[jj];
+            continue;
+        }
+        const double l = quad_bcast(w[c >> 2] * cself[c], c & 3);  // 0 from column nbt on
         const double* wd = &WdS[c][q][0];
 #pragma unroll
         for (int jj = c >> 2; jj < kAppNB / 4; ++jj) w[jj] -= l * wd[jj];  // W(., c) = 0 at columns <= c
@@ -3617,17 +3714,31 @@ __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* _
     // every block's maxima are in: the a-posteriori test and the commit
     const unsigned long long cm = lane < nbt ? __hip_atomic_load(&sl->cmax[lane], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
     const double dd = lane < nbt ? sl->d[lane] : 0.0;
-    const unsigned long long bad = __ballot(lane < nbt && A.u * as_double(cm) > fabs(dd));
-    const int nacc = bad ? (int)__builtin_ctzll(bad) : nbt;
+    const int kind = lane < nbt ? (int)sl->kind[lane] : PIV_1X1;
+    const double off = lane < nbt ? sl->offd[lane] : 0.0;
+    // 2x2 pairs: the test of k_app_diag again with the maxima over every row below the pair
+    const double g = as_double(cm), gn = __shfl(g, lane < 63 ? lane + 1 : lane), dn = __shfl(dd, lane < 63 ? lane + 1 : lane);
+    const double det = dd * dn - off * off;
+    const double lim = fabs(det) / A.u;
+    const bool badA = !(det != 0.0 && fabs(dn) * g + fabs(off) * gn <= lim && fabs(off) * g + fabs(dd) * gn <= lim);
+    const bool badAprev = __shfl(badA, lane > 0 ? lane - 1 : 0);
+    const bool bad1 = kind == PIV_2X2_A ? badA : kind == PIV_2X2_B ? badAprev : A.u * g > fabs(dd);
+    const unsigned long long bad = __ballot(lane < nbt && bad1);
+    const int nacc = bad ? (int)__builtin_ctzll(bad) : nbt;  // a failing pair fails at its first column
     const bool acc = lane < nacc;
-    if (acc) A.piv[A.rows_off[f] + k0 + lane] = PIV_1X1;
-    const int npos = (int)__popcll(__ballot(acc && dd > 0.0));
-    double mn = acc ? fabs(dd) : INFINITY;
+    if (acc) A.piv[A.rows_off[f] + k0 + lane] = (int8_t)kind;
+    // inertia: a 1x1 by its sign; a pair by det < 0 (one each) or the sign of its trace (both)
+    const int npos = (int)__popcll(__ballot(acc && kind == PIV_1X1 && dd > 0.0)) +
+                     (int)__popcll(__ballot(acc && kind == PIV_2X2_A && det < 0.0)) +
+                     2 * (int)__popcll(__ballot(acc && kind == PIV_2X2_A && det > 0.0 && dd + dn > 0.0));
+    const int n2 = (int)__popcll(__ballot(acc && kind == PIV_2X2_A));
+    double mn = acc ? (kind == PIV_1X1 ? fabs(dd) : fmax(fabs(dd), fabs(off))) : INFINITY;
     for (int o = 32; o > 0; o >>= 1) mn = fmin(mn, __shfl_xor(mn, o));
     if (lane == 0) {
         BigFrontState S = A.big[f];
         S.npos += npos;
         S.nneg += nacc - npos;
+        S.n2 += n2;
         S.minpiv = fmin(S.minpiv, mn);
         S.k = k0 + nacc;
         S.k0 = S.k;
@@ -3722,7 +3833,8 @@ __global__ __launch_bounds__(512) void k_app_exact(FactorArgs A, const int32_t* 
 __global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int32_t* __restrict__ fronts, int tiles_max) {
     __shared__ __attribute__((aligned(16))) double As[kAppNB][64 + 2];  // -L(i0t + r, q) at [q][r]
     __shared__ __attribute__((aligned(16))) double Bs[kAppNB][64 + 2];  //  W(j0t + c, q) at [q][c]
-    __shared__ double dinv[kAppNB];
+    __shared__ double cself[kAppNB], coth[kAppNB];                     // app_coefs
+    __shared__ int partner[kAppNB];
     const int f = fronts[blockIdx.y];
     const int m = A.fm[f];
     const AppSlot* sl = app_slot(A, f, m);
@@ -3746,12 +3858,13 @@ __global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int
     int ti, tj;
     tri_rc((int)blockIdx.x, ti, tj);
     const int i0t = u0 + 64 * ti, j0t = u0 + 64 * tj;
-    if (tid < kAppNB) dinv[tid] = tid < nacc ? 1.0 / sl->d[tid] : 0.0;
+    if (tid < kAppNB) app_coefs(sl, tid, nacc, cself[tid], coth[tid], partner[tid]);
     __syncthreads();
     for (int t = tid; t < 64 * kAppNB; t += kThreads) {
         const int r = t >> 6, q = t & 63;
         const int i = i0t + r, j = j0t + r;
-        As[q][r] = (i < m && q < nacc) ? -(P[(int64_t)(i - k0) * kAppNB + q] * dinv[q]) : 0.0;
+        const double* Pi = P + (int64_t)(i - k0) * kAppNB;
+        As[q][r] = (i < m && q < nacc) ? -(cself[q] * Pi[q] + coth[q] * Pi[partner[q]]) : 0.0;
         Bs[q][r] = (j < m && q < nacc) ? P[(int64_t)(j - k0) * kAppNB + q] : 0.0;
     }
     const int lane = tid & 63, w = tid >> 6;

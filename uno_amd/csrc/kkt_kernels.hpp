@@ -22,13 +22,16 @@ struct BigFrontState {
 // global scratch holds, after its m x m front, the step's panel (m x kAppNB, row-major) and an AppSlot
 constexpr int kAppNB = 64;
 struct AppSlot {
-    unsigned long long cmax[kAppNB];  // max |W(i, c)| over the rows below the diagonal (bits; atomic max)
-    double d[kAppNB];                 // the diagonal block's pivots
+    unsigned long long cmax[kAppNB];  // max |W(i, c)| over the rows below the diagonal (bits; atomic max); for a
+                                      // 2x2 pair, over the rows below the pair
+    double d[kAppNB];                 // the diagonal block's pivots (a 2x2 pair: its two diagonal entries)
+    double offd[kAppNB];              // a 2x2 pair's off-diagonal entry (both columns)
+    int8_t kind[kAppNB];              // PIV_1X1, PIV_2X2_A / PIV_2X2_B (pair with the next / previous column)
     int32_t k0, nbt, nacc, nb;        // first column, columns passing the in-block test, accepted, block width
     uint32_t arrive;                  // k_app_rows blocks done (the last one decides nacc)
     int32_t pad_[3];
 };
-constexpr int64_t kAppSlotDoubles = 160;
+constexpr int64_t kAppSlotDoubles = 208;
 static_assert(sizeof(AppSlot) <= kAppSlotDoubles * sizeof(double), "AppSlot");
 
 // Arguments of the front factorization kernels (device pointers, SoA per front).
