@@ -3673,23 +3673,22 @@ __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* _
     double w[kAppNB / 4];
 #pragma unroll
     for (int jj = 0; jj < kAppNB / 4; ++jj) w[jj] = (valid && 4 * jj + q < nbt) ? row[4 * jj + q] : 0.0;
+    // one update body per column (the code stays within the instruction cache): L(i, c) = cself W(i, c) +
+    // coth W(i, partner).  A pair's columns are applied one after the other: column c's update does not touch
+    // W(i, c + 1) (the pair row is zero in WdS[c]) and no update touches columns <= c, so both L(i, .) of the
+    // pair see the W values of the pair's start.
 #pragma unroll
     for (int c = 0; c < kAppNB; ++c) {
         const int kc = kindS[c];  // uniform
-        if (kc == PIV_2X2_B) continue;  // applied with its first column
-        if (c + 1 < kAppNB && kc == PIV_2X2_A) {
-            const double wc = quad_bcast(w[c >> 2], c & 3), wr = quad_bcast(w[(c + 1) >> 2], (c + 1) & 3);
-            const double l0 = cself[c] * wc + coth[c] * wr, l1 = cself[c + 1] * wr + coth[c + 1] * wc;
-            const double* wd0 = &WdS[c][q][0];
-            const double* wd1 = &WdS[c + 1][q][0];
-#pragma unroll
-            for (int jj = c >> 2; jj < kAppNB / 4; ++jj) w[jj] -= l0 * wd0[jj] + l1 * wd1[jj];
-            continue;
-        }
-        const double l = quad_bcast(w[c >> 2] * cself[c], c & 3);  // 0 from column nbt on
+        const double wc = quad_bcast(w[c >> 2], c & 3);
+        const double wa = quad_bcast(w[(c + 1 < kAppNB ? c + 1 : c) >> 2], (c + 1) & 3);
+        const double wb = quad_bcast(w[(c > 0 ? c - 1 : c) >> 2], (c + 3) & 3);
+        const double wp = kc == PIV_2X2_A ? wa : (kc == PIV_2X2_B ? wb : 0.0);
+        const double l = cself[c] * wc + coth[c] * wp;  // 0 from column nbt on
         const double* wd = &WdS[c][q][0];
 #pragma unroll
         for (int jj = c >> 2; jj < kAppNB / 4; ++jj) w[jj] -= l * wd[jj];  // W(., c) = 0 at columns <= c
+        __asm__ volatile("" ::: "memory");  // the next column's LDS operands are not hoisted above this one
     }
     if (valid) {
         double* pw = P + (int64_t)(i - k0) * kAppNB;
