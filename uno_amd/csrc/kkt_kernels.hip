@@ -3832,8 +3832,6 @@ __global__ __launch_bounds__(512) void k_app_exact(FactorArgs A, const int32_t* 
 __global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int32_t* __restrict__ fronts, int tiles_max) {
     __shared__ __attribute__((aligned(16))) double As[kAppNB][64 + 2];  // -L(i0t + r, q) at [q][r]
     __shared__ __attribute__((aligned(16))) double Bs[kAppNB][64 + 2];  //  W(j0t + c, q) at [q][c]
-    __shared__ double cself[kAppNB], coth[kAppNB];                     // app_coefs
-    __shared__ int partner[kAppNB];
     const int f = fronts[blockIdx.y];
     const int m = A.fm[f];
     const AppSlot* sl = app_slot(A, f, m);
@@ -3857,14 +3855,24 @@ __global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int
     int ti, tj;
     tri_rc((int)blockIdx.x, ti, tj);
     const int i0t = u0 + 64 * ti, j0t = u0 + 64 * tj;
-    if (tid < kAppNB) app_coefs(sl, tid, nacc, cself[tid], coth[tid], partner[tid]);
-    __syncthreads();
-    for (int t = tid; t < 64 * kAppNB; t += kThreads) {
-        const int r = t >> 6, q = t & 63;
-        const int i = i0t + r, j = j0t + r;
+    // the panel staging: thread t stages column q = t % 64 of rows t / 64 + 4 u (its coefficients formed by
+    // itself, no barrier before); every load is issued before the first LDS write (one memory round trip,
+    // not one per row), and the C tile's loads go out with them
+    static_assert(kThreads == 4 * kAppNB, "staging: 4 rows x 64 columns per pass");
+    constexpr int SR = 64 / (kThreads / kAppNB);  // rows per thread
+    const int q = tid & 63, r0 = tid >> 6;
+    double cs, co;
+    int pt;
+    app_coefs(sl, q, nacc, cs, co, pt);
+    double pa[SR], pb[SR], pc[SR];
+#pragma unroll
+    for (int u = 0; u < SR; ++u) {
+        const int r = r0 + 4 * u;
+        const int i = min(i0t + r, m - 1), j = min(j0t + r, m - 1);  // clamped: rows past m stage zeros below
         const double* Pi = P + (int64_t)(i - k0) * kAppNB;
-        As[q][r] = (i < m && q < nacc) ? -(cself[q] * Pi[q] + coth[q] * Pi[partner[q]]) : 0.0;
-        Bs[q][r] = (j < m && q < nacc) ? P[(int64_t)(j - k0) * kAppNB + q] : 0.0;
+        pa[u] = Pi[q];
+        pb[u] = Pi[pt];
+        pc[u] = P[(int64_t)(j - k0) * kAppNB + q];
     }
     const int lane = tid & 63, w = tid >> 6;
     const int lr = lane & 15, lk = lane >> 4;
@@ -3879,14 +3887,20 @@ __global__ __launch_bounds__(kThreads) void k_app_update(FactorArgs A, const int
             acc[c][r] = (i < m && j < m && j <= i) ? st.at(i, j) : 0.0;
         }
     }
+#pragma unroll
+    for (int u = 0; u < SR; ++u) {
+        const int r = r0 + 4 * u;
+        As[q][r] = (i0t + r < m && q < nacc) ? -(cs * pa[u] + co * pb[u]) : 0.0;
+        Bs[q][r] = (j0t + r < m && q < nacc) ? pc[u] : 0.0;
+    }
     __syncthreads();
     const bool diag = ti == tj;
-    for (int q = 0; q < nacc; q += 4) {
-        const double a = As[q + lk][16 * w + lr];
+    for (int qq = 0; qq < nacc; qq += 4) {
+        const double a = As[qq + lk][16 * w + lr];
 #pragma unroll
         for (int c = 0; c < 4; ++c) {
             if (diag && c > w) continue;  // wave-uniform: strip entirely above the diagonal
-            const double b = Bs[q + lk][16 * c + lr];
+            const double b = Bs[qq + lk][16 * c + lr];
             acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc[c], 0, 0, 0);
         }
     }
