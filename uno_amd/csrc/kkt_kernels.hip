@@ -3655,10 +3655,18 @@ __global__ __launch_bounds__(256) void k_app_rows(FactorArgs A, const int32_t* _
     const int k0 = sl->k0;
     double* P = app_panel(A, f, m);
     // the pair's second row (W(c + 1, c) = its off-diagonal) is not an update operand of the pair's columns
-    for (int t = tid; t < kAppNB * kAppNB; t += 256) {
-        const int j = t >> 6, c = t & 63;
-        const bool pairrow = c < nbt && j == c + 1 && sl->kind[c] == PIV_2X2_A;
-        WdS[c][j & 3][j >> 2] = (c < j && j < nbt && !pairrow) ? P[(int64_t)j * kAppNB + c] : 0.0;
+    // thread t stages column c = t % 64 of rows t / 64 + 4 u: every load issued before the first LDS write
+    {
+        const int c = tid & 63, j0 = tid >> 6;
+        const bool pairc = c < nbt && sl->kind[c] == PIV_2X2_A;
+        double v[kAppNB / 4];
+#pragma unroll
+        for (int u = 0; u < kAppNB / 4; ++u) v[u] = P[(int64_t)(j0 + 4 * u) * kAppNB + c];
+#pragma unroll
+        for (int u = 0; u < kAppNB / 4; ++u) {
+            const int j = j0 + 4 * u;
+            WdS[c][j & 3][j >> 2] = (c < j && j < nbt && !(pairc && j == c + 1)) ? v[u] : 0.0;
+        }
     }
     if (tid < kAppNB) {
         int pt;
