@@ -105,33 +105,72 @@ def run_ipm(args):
         retries += nf - 1
         its.append(list(inertia))
     st = kkt.stats()
-    # the same sequence device-resident: iterate and values in HBM, Sigma assembled by
-    # uno_kkt_assemble_barrier from x, zl, zu (PrimalDualInteriorPointProblem.cpp:56-78), retries edit the
-    # regularization diagonal on the device, rhs / solution device pointers: no host transfer in the loop
+    # the same sequence device-resident: the iterate (x, zl, zu, y) lives in HBM and every
+    # value of every iteration is produced on the device -- the model's gradient and constraints (torch on the
+    # resident band / Jacobian terms: the model's part), the augmented KKT values by uno_kkt_assemble_augmented
+    # (regularization zeros, sigma * H, Sigma from x / zl / zu, J: Subproblem::assemble_augmented_matrix), the
+    # inertia-correction retries by uno_kkt_fill_values, the right-hand side by uno_kkt_assemble_rhs
+    # (Subproblem.cpp:80-99), the solve on device vectors, then the primal-dual direction and the
+    # fraction-to-boundary step lengths by uno_kkt_assemble_direction (PrimalDualInteriorPointProblem.cpp:173-325).
+    # Nothing crosses PCIe but the inertia (3 integers) and the two step lengths.
     dev = torch.device("cuda", 0)
     kd = uno_amd.HipKKT(0, delay_relaxed=0)
     kd.analyze(n, rows, cols)
     lbv, ubv = np.full(nv, -10.0), np.full(nv, 10.0)
     assert kd.barrier_setup(lbv, ubv) == nv
-    vd = torch.from_numpy(np.array(vals)).to(dev)
-    bd = torch.from_numpy(np.array(rhs)).to(dev)
-    xd_sol = torch.empty_like(bd)
+    nj = len(vals) - (n + nh + nv)
+    kd.augmented_setup(n, nh, nj)
+    jrow = np.asarray(rows[n + nh + nv:], dtype=np.int64)            # J^T entries (var, nv + j), constraint-major
+    jcol = np.asarray(cols[n + nh + nv:], dtype=np.int64) - nv
+    kd.rhs_setup(nv, m, jcol, jrow)
+    T = lambda a, dt=torch.float64: torch.from_numpy(np.ascontiguousarray(a)).to(dev, dt)
+    hess_d = T(np.asarray(vals[n:n + nh]))                           # the model's Hessian terms (H of the QP)
+    jac_d = T(np.asarray(vals[n + nh + nv:]))
+    hr, hc = T(np.asarray(rows[n:n + nh]), torch.int64), T(np.asarray(cols[n:n + nh]), torch.int64)
+    hoff = torch.nonzero(hr != hc).flatten()            # off-diagonal Hessian terms (gathered once)
+    hr_off, hc_off = hr[hoff].contiguous(), hc[hoff].contiguous()
+    jr_d, jc_d = T(jrow, torch.int64), T(jcol, torch.int64)
+    lb_d, ub_d = T(lbv), T(ubv)
+    vd = torch.empty(len(vals), dtype=torch.float64, device=dev)
+    gvec = torch.empty(nv, dtype=torch.float64, device=dev)
+    grad, cons = torch.empty_like(gvec), torch.empty(m, dtype=torch.float64, device=dev)
+    rhs_d = torch.empty(n, dtype=torch.float64, device=dev)
+    sol_d = torch.empty_like(rhs_d)
     xs = torch.empty(nv, dtype=torch.float64, device=dev)
-    zl = torch.empty_like(xs)
-    zu = torch.empty_like(xs)
+    zl, zu = torch.empty_like(xs), torch.empty_like(xs)
+    yv = torch.empty(m, dtype=torch.float64, device=dev)
+    dx, dzl, dzu = torch.empty_like(xs), torch.empty_like(xs), torch.empty_like(xs)
+    dy = torch.empty_like(yv)
     gen = torch.Generator(device=dev)
     gen.manual_seed(11)
+    gvec.uniform_(-1.0, 1.0, generator=gen)
     torch.cuda.synchronize()
-    t_dev, facs_d = [], 0
+    t_dev, facs_d, steps_d = [], 0, []
+    t_asm, t_model = [], []
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    stream = torch.cuda.ExternalStream(kd.stream())
     for it in range(args.ipm_iters + 1):
         # a new interior point: x inside the box, bound multipliers of the late-IPM spread
         xs.uniform_(-9.0, 9.0, generator=gen)
         zl.copy_(10.0 ** (torch.rand(nv, dtype=torch.float64, device=dev, generator=gen) * 16 - 8))
         zu.copy_(-(10.0 ** (torch.rand(nv, dtype=torch.float64, device=dev, generator=gen) * 16 - 8)))
+        yv.uniform_(-1.0, 1.0, generator=gen)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        kd.assemble_barrier(xs.data_ptr(), zl.data_ptr(), zu.data_ptr(), vd.data_ptr() + 8 * sig0)
-        kd.fill_values(0, n, 0.0) if it else None
+        # model evaluation on the device (ArrowbandModel: gradient H x + g, constraints A x - b with b = 0 here)
+        grad.copy_(gvec)
+        grad.index_add_(0, hr, hess_d * xs[hc])
+        grad.index_add_(0, hc_off, hess_d[hoff] * xs[hr_off])
+        cons.zero_()
+        cons.index_add_(0, jc_d, jac_d * xs[jr_d])
+        torch.cuda.current_stream().synchronize()
+        t_model.append(time.perf_counter() - t0)
+        with torch.cuda.stream(stream):
+            ev[0].record(stream)
+        kd.assemble_augmented(1.0, hess_d.data_ptr(), jac_d.data_ptr(), xs.data_ptr(), zl.data_ptr(), zu.data_ptr(),
+                              vd.data_ptr())
+        with torch.cuda.stream(stream):
+            ev[1].record(stream)
         kd.factorize(device_ptr=vd.data_ptr())
         inertia = kd.inertia()
         nf, dw = 1, 0.0
@@ -142,11 +181,28 @@ def run_ipm(args):
             kd.factorize()
             inertia = kd.inertia()
             nf += 1
-        kd.solve_device(bd.data_ptr(), xd_sol.data_ptr())
+        kd.assemble_rhs(grad.data_ptr(), cons.data_ptr(), yv.data_ptr(), jac_d.data_ptr(), rhs_d.data_ptr())
+        kd.solve_device(rhs_d.data_ptr(), sol_d.data_ptr())
+        ap, ad = kd.assemble_direction(nv, m, sol_d.data_ptr(), xs.data_ptr(), lb_d.data_ptr(), ub_d.data_ptr(),
+                                       zl.data_ptr(), zu.data_ptr(), 1e-6, 0.99, dx.data_ptr(), dy.data_ptr(),
+                                       dzl.data_ptr(), dzu.data_ptr())
         torch.cuda.synchronize()
         if it:  # the first pass warms up
             t_dev.append(time.perf_counter() - t0)
+            t_asm.append(ev[0].elapsed_time(ev[1]))
             facs_d += nf
+            steps_d.append([ap, ad])
+    # the device-assembled values of the last iteration against the host restatement of the same assembly
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    asm_check = None
+    if os.path.exists(os.path.join(ROOT, "oracle", "ipm_oracle.py")):
+        import ipm_oracle
+        # the last iteration's values after its retries: the regularization prefix holds delta_w / -delta_c
+        # (uno_kkt_fill_values), every other position the assembly's value
+        ref = ipm_oracle.assemble_augmented(n, 1.0, np.asarray(vals[n:n + nh]), np.asarray(vals[n + nh + nv:]),
+                                            xs.cpu().numpy(), lbv, ubv, zl.cpu().numpy(), zu.cpu().numpy())
+        got = vd.cpu().numpy()
+        asm_check = bool(np.array_equal(got[n:].view(np.uint64), ref[n:].view(np.uint64)))
     res = np.abs(uno_amd.coo_symv(n, rows, cols, v, x) - rhs).max()
     absk = uno_amd.coo_symv(n, rows, cols, np.abs(v), np.ones(n)).max()
     total = sum(t_it)
@@ -159,8 +215,15 @@ def run_ipm(args):
         "device_resident": {"factorizations_per_s": round(facs_d / sum(t_dev), 3), "factorizations": facs_d,
                             "ms_per_iteration_median": round(1e3 * float(np.median(t_dev)), 3),
                             "ms_per_factorization": round(1e3 * sum(t_dev) / facs_d, 3),
-                            "note": "Sigma assembled on the device (uno_kkt_assemble_barrier), retries by "
-                                    "uno_kkt_fill_values, device rhs / solution: no PCIe in the loop"},
+                            "model_eval_ms_median": round(1e3 * float(np.median(t_model)), 3),
+                            "assemble_augmented_ms_median": round(float(np.median(t_asm)), 4),
+                            "assemble_augmented_GBs": round((8.0 * (len(vals) + nh + nj) + 45.0 * nv) / (float(np.median(t_asm)) * 1e-3) / 1e9, 1),
+                            "assembly_bit_identical_to_oracle": asm_check,
+                            "step_lengths_last": steps_d[-1] if steps_d else None,
+                            "note": "per iteration on the device: model gradient / constraints (torch), augmented KKT "
+                                    "values (uno_kkt_assemble_augmented: zeros, sigma*H, Sigma, J), delta_w retries "
+                                    "(uno_kkt_fill_values), rhs (uno_kkt_assemble_rhs), solve, direction + "
+                                    "fraction-to-boundary (uno_kkt_assemble_direction): no value crosses PCIe"},
         "rel_residual_last": float(res / (absk * np.abs(x).max() + np.abs(rhs).max())),
         "config": {"workload": "C3 arrowband KKT, Sigma redrawn per iteration, delta_w retries, host values + rhs",
                    "n": n, "nnz": len(vals), "full_upload_bytes": 8 * len(vals), "retry_upload_bytes": 8 * n},

@@ -167,6 +167,23 @@ int uno_kkt_barrier_setup(uno_kkt_t handle, int64_t n_vars, const double* lb, co
 int64_t uno_kkt_barrier_count(uno_kkt_t handle);
 int uno_kkt_assemble_barrier(uno_kkt_t handle, const double* x, const double* zl, const double* zu, double* values);
 
+/* Augmented (KKT) values on the device, Subproblem::assemble_augmented_matrix (uno/ingredients/subproblem/
+ * Subproblem.cpp:57-70) with PrimalDualInteriorPointProblem::evaluate_lagrangian_hessian (:56-78) and COOFormat's
+ * regularization-first layout (COOFormat.hpp:78-99): the whole COO value array in Uno's insertion order,
+ *   values[0, reg_size)                             = 0 (the regularization diagonal after COOFormat::reset)
+ *   values[reg_size + k], k < nnz_hess               = hess_scale * hess[k]: the model's Lagrangian Hessian terms in
+ *                                                      its insertion order (upper triangle, column-major for an
+ *                                                      AMPL-like model); hess_scale = the objective multiplier for a
+ *                                                      model with linear constraints (Hessian sigma * H), else 1
+ *   values[reg_size + nnz_hess + t], t < barrier_count = Sigma_t as uno_kkt_assemble_barrier
+ *   values[reg_size + nnz_hess + barrier_count + e]  = jac[e]: Jacobian entries constraint-major (Subproblem.cpp:64-69)
+ * bit-identical to the host assembly.  uno_kkt_augmented_setup (after uno_kkt_barrier_setup) fixes the segment
+ * lengths, checked against the analysed nnz.  DEVICE pointers; queued on the solver's stream, so a following
+ * uno_kkt_factorize(h, values, 1) sees them: with the iterate in HBM no value crosses PCIe. */
+int uno_kkt_augmented_setup(uno_kkt_t handle, int64_t reg_size, int64_t nnz_hess, int64_t nnz_jac);
+int uno_kkt_assemble_augmented(uno_kkt_t handle, double hess_scale, const double* hess, const double* jac, const double* x,
+                               const double* zl, const double* zu, double* values);
+
 /* Primal-dual direction, PrimalDualInteriorPointProblem::assemble_primal_dual_direction
  * (PrimalDualInteriorPointProblem.cpp:173-194) with compute_bound_dual_direction (:262-278) and the
  * fraction-to-boundary rules (:281-325), tau = max(tau_min, 1 - barrier_parameter): dx = sol[0:n],

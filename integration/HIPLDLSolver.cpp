@@ -47,6 +47,44 @@ namespace uno {
          return uno_kkt_stage_values(static_cast<uno_kkt_t>(h), v, first, count);
       }
       const char* hip_last_error(void* h) { return uno_kkt_last_error(static_cast<uno_kkt_t>(h)); }
+
+      // UNO_HIPLDL_PROFILE_ASSEMBLY=1 (profiling runs only): the assembly is run a second time into this matrix,
+      // whose insert keeps nothing, so the driver's host profile can split Subproblem::assemble_augmented_matrix
+      // into the model evaluation with Uno's assembly loops and virtual dispatch (this pass) and the storage
+      // cost of the plugin's matrix (the difference)
+      class DiscardingMatrix : public SymmetricMatrix<size_t, double> {
+      public:
+         DiscardingMatrix(size_t n, size_t cap): n(n), cap(cap) {}
+         void reset() override { this->nnz = 0; }
+         [[nodiscard]] size_t dimension() const override { return this->n; }
+         [[nodiscard]] size_t number_nonzeros() const override { return this->nnz; }
+         [[nodiscard]] size_t capacity() const override { return this->cap; }
+         void insert(size_t row_index, size_t column_index, double term) override {
+            this->sink += term + static_cast<double>(row_index ^ column_index);  // keeps the arguments live
+            this->nnz++;
+         }
+         void finalize_column(size_t) override {}
+         [[nodiscard]] double smallest_diagonal_entry(size_t) const override { return 0.; }
+         void set_regularization(const Collection<size_t>&, size_t, double) override {}
+         [[nodiscard]] const double* data_pointer() const noexcept override { return &this->sink; }
+         [[nodiscard]] double* data_pointer() noexcept override { return &this->sink; }
+         double sink{0.};
+      protected:
+         [[nodiscard]] std::tuple<size_t, size_t, double> dereference_iterator(size_t, size_t) const override { return {0, 0, 0.}; }
+         void increment_iterator(size_t& column_index, size_t& nonzero_index) const override {
+            nonzero_index++;
+            if (nonzero_index == this->nnz) column_index = this->n;
+         }
+      private:
+         size_t n, cap, nnz{0};
+      };
+      bool profile_assembly() {
+         static const bool on = [] {
+            const char* env = std::getenv("UNO_HIPLDL_PROFILE_ASSEMBLY");
+            return env != nullptr && std::atoi(env) != 0;
+         }();
+         return on;
+      }
    } // namespace
 
    const KKTBackend& hip_kkt_backend() {
@@ -102,6 +140,10 @@ namespace uno {
       }
       this->dimension = matrix.dimension();
       this->analysed_nonzeros = matrix.number_nonzeros();
+      if (&matrix == &this->augmented_matrix) {
+         // the pattern is fixed from now on (SURVEY.md 8(b) invariant 1): later assemblies store values only
+         this->augmented_matrix.freeze_pattern();
+      }
       this->check(this->backend.analyze(this->handle, static_cast<int64_t>(matrix.dimension()),
          static_cast<int64_t>(this->row_indices.size()), this->row_indices.data(), this->column_indices.data()), "analyze");
       // from now on the plugin's matrix streams its values to the device as Uno inserts them (chunks of
@@ -178,6 +220,16 @@ namespace uno {
          this->augmented_matrix.reset();
          subproblem.assemble_augmented_matrix(statistics, this->augmented_matrix, this->constraint_jacobian);
          prof.assemble += seconds_since(t0);
+         if (profile_assembly()) {
+            DiscardingMatrix discard(this->dimension, this->augmented_matrix.capacity());
+            t0 = std::chrono::steady_clock::now();
+            subproblem.assemble_augmented_matrix(statistics, discard, this->constraint_jacobian);
+            prof.assemble_model += seconds_since(t0);
+            prof.assemble_profiled++;
+            if (discard.number_nonzeros() + this->regularization_size != this->augmented_matrix.number_nonzeros()) {
+               throw std::runtime_error("HIPLDL: the profiling assembly inserted a different number of entries");
+            }
+         }
          this->values_fresh = true;
          struct Scope {  // also reset when the loop throws (UnstableRegularization, FeasibilityRestoration.cpp:103-105)
             bool& flag;

@@ -39,6 +39,9 @@ namespace kkt_trace {
    struct Profile {
       double evaluate{0.0};     // objective gradient, constraints, Jacobian (Subproblem::evaluate_*)
       double assemble{0.0};     // Subproblem::assemble_augmented_matrix (COO inserts into the plugin's matrix)
+      double assemble_model{0.0};  // UNO_HIPLDL_PROFILE_ASSEMBLY=1: the same assembly into a discarding matrix (model
+                                   // evaluation + Uno's loops + virtual insert calls; assemble - this = storage)
+      size_t assemble_profiled{0};
       double regularize{0.0};   // Subproblem::regularize_augmented_matrix: inertia-correction loop, factorizations
       double factorize{0.0};    //   of which: the plugin's factorize + inertia calls (device work + value upload)
       double rhs{0.0};          // Subproblem::assemble_augmented_rhs

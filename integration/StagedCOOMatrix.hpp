@@ -8,20 +8,28 @@
 // same order -- so the analysed pattern, the values the solver factors and every Uno-side query are those of
 // the MUMPS adapter's matrix (MUMPSSolver.hpp:52).
 //
-// What differs is the upload: after every `chunk` inserted entries the new range is handed to a stager
-// (the plugin binds uno_kkt_stage_values, an asynchronous host-to-device copy on its own stream), so the
-// PCIe transfer of the ~160 MB of values at configs[2] runs under Uno's assembly of the later entries
-// instead of after it.  flush() stages the tail and, when set_regularization touched them, the
-// regularization positions again; the factorization then reads the device copy (uno_kkt_factorize(h,
-// NULL, 0)).  The value storage is reserved once at the full capacity (stable address: the library may
-// page-lock it, option pin_host_values).
+// What differs:
+// - the upload: after every `chunk` inserted entries the new range is handed to a stager (the plugin binds
+//   uno_kkt_stage_values, an asynchronous host-to-device copy on its own stream), so the PCIe transfer of the
+//   ~160 MB of values at configs[2] runs under Uno's assembly of the later entries instead of after it.
+//   flush() stages the tail and, when set_regularization touched them, the regularization positions again;
+//   the factorization then reads the device copy (uno_kkt_factorize(h, NULL, 0)).
+// - the insert after the symbolic analysis: the pattern is fixed from then on (SURVEY.md 8(b) invariant 1,
+//   PrimalDualRegularization.hpp:145-149 analyses once), so freeze_pattern() keeps the analysed row / column
+//   indices and every later insert stores only its value -- one store into the (page-locked) value array,
+//   no row / column push_back and no capacity growth.  Option UNO_HIPLDL_CHECK_PATTERN=1 (tests) compares
+//   each insert's indices with the frozen pattern and throws on a difference.
+// The value storage is allocated once at the full capacity (stable address: the library may page-lock it,
+// option pin_host_values).
 #ifndef UNO_STAGEDCOOMATRIX_H
 #define UNO_STAGEDCOOMATRIX_H
 
 #include <algorithm>
 #include <cstddef>
+#include <cstdlib>
 #include <functional>
 #include <stdexcept>
+#include <string>
 #include <tuple>
 #include <vector>
 
@@ -37,9 +45,11 @@ namespace uno {
       StagedCOOMatrix() = default;
       StagedCOOMatrix(size_t dimension, size_t capacity, size_t regularization_size):
             SymmetricMatrix<size_t, double>(), n(dimension), cap(capacity + regularization_size), reg_size(regularization_size) {
-         this->values.reserve(this->cap);
+         this->values.assign(this->cap, 0.0);
          this->rows.reserve(this->cap);
          this->cols.reserve(this->cap);
+         const char* env = std::getenv("UNO_HIPLDL_CHECK_PATTERN");
+         this->check_pattern = env != nullptr && std::atoi(env) != 0;
          this->reset();
       }
       StagedCOOMatrix& operator=(StagedCOOMatrix&& other) = default;
@@ -52,6 +62,15 @@ namespace uno {
          this->reg_dirty = true;
       }
       [[nodiscard]] bool staging() const { return static_cast<bool>(this->stager); }
+
+      // the symbolic analysis saw the entries present now: from here on inserts store values only
+      void freeze_pattern() {
+         this->rows.resize(this->nnz);
+         this->cols.resize(this->nnz);
+         this->frozen_nnz = this->nnz;
+         this->frozen = true;
+      }
+      [[nodiscard]] bool pattern_frozen() const { return this->frozen; }
 
       // stage what has not been staged since reset(): the tail, and the regularization positions if edited
       void flush() {
@@ -67,12 +86,16 @@ namespace uno {
       // SymmetricMatrix interface (COOFormat semantics)
       void reset() override {
          this->nnz = 0;
-         this->values.clear();
-         this->rows.clear();
-         this->cols.clear();
          this->staged = 0;
-         this->reg_dirty = false;
-         for (size_t i = 0; i < this->reg_size; ++i) this->push(i, i, 0.0);  // COOFormat::initialize_regularization
+         if (!this->frozen) {
+            this->rows.clear();
+            this->cols.clear();
+            for (size_t i = 0; i < this->reg_size; ++i) this->push(i, i, 0.0);  // COOFormat::initialize_regularization
+         }
+         else {
+            std::fill(this->values.begin(), this->values.begin() + static_cast<std::ptrdiff_t>(this->reg_size), 0.0);
+            this->nnz = this->reg_size;
+         }
          this->reg_dirty = true;  // set_regularization fills them later: staged at flush()
          this->staged = this->nnz;
       }
@@ -81,7 +104,18 @@ namespace uno {
       [[nodiscard]] size_t capacity() const override { return this->cap; }
 
       void insert(size_t row_index, size_t column_index, double term) override {
-         this->push(row_index, column_index, term);
+         if (this->frozen) {
+            if (this->nnz >= this->frozen_nnz) {
+               throw std::length_error("StagedCOOMatrix: more entries than the analysed pattern");
+            }
+            if (this->check_pattern && (this->rows[this->nnz] != row_index || this->cols[this->nnz] != column_index)) {
+               throw std::logic_error("StagedCOOMatrix: entry " + std::to_string(this->nnz) + " differs from the analysed pattern");
+            }
+            this->values[this->nnz++] = term;
+         }
+         else {
+            this->push(row_index, column_index, term);
+         }
          if (this->stager && this->nnz - this->staged >= this->chunk) {
             this->stager(this->values.data(), this->staged, this->nnz - this->staged);
             this->staged = this->nnz;
@@ -109,18 +143,21 @@ namespace uno {
 
    protected:
       size_t n{0}, cap{0}, reg_size{0}, nnz{0};
-      std::vector<double> values{};
-      std::vector<size_t> rows{}, cols{};
+      std::vector<double> values{};          // cap entries, allocated once (stable address)
+      std::vector<size_t> rows{}, cols{};    // the pattern (frozen after the analysis)
       Stager stager{};
       size_t chunk{1};
       size_t staged{0};       // values[0, staged) handed to the stager since reset()
       bool reg_dirty{false};  // regularization positions to stage (again) at flush()
+      bool frozen{false};
+      size_t frozen_nnz{0};
+      bool check_pattern{false};
 
       void push(size_t row_index, size_t column_index, double term) {
          if (this->nnz >= this->cap) {
             throw std::length_error("StagedCOOMatrix: capacity exceeded");  // the address must stay stable
          }
-         this->values.push_back(term);
+         this->values[this->nnz] = term;
          this->rows.push_back(row_index);
          this->cols.push_back(column_index);
          this->nnz++;

@@ -313,8 +313,14 @@ int main(int argc, char* argv[]) {
          const double plugin = pr.evaluate + pr.assemble + pr.regularize + pr.rhs + pr.solve + pr.direction;
          std::printf("], \"host_profile_s\": {\"wall\": %.6f, \"plugin_orchestration\": %.6f, \"evaluate\": %.6f, "
             "\"assemble_coo\": %.6f, \"regularize\": %.6f, \"factorize_inertia\": %.6f, \"rhs\": %.6f, \"solve\": %.6f, "
-            "\"direction\": %.6f, \"uno_core_outside_plugin\": %.6f, \"orchestration_calls\": %zu}", wall, plugin, pr.evaluate,
+            "\"direction\": %.6f, \"uno_core_outside_plugin\": %.6f, \"orchestration_calls\": %zu", wall, plugin, pr.evaluate,
             pr.assemble, pr.regularize, pr.factorize, pr.rhs, pr.solve, pr.direction, wall - plugin, pr.calls);
+         if (pr.assemble_profiled > 0) {  // UNO_HIPLDL_PROFILE_ASSEMBLY=1: assemble_coo split (the second pass is
+                                          // outside plugin_orchestration and inside uno_core_outside_plugin)
+            std::printf(", \"assemble_split\": {\"assemblies\": %zu, \"model_and_uno_loops\": %.6f, \"plugin_storage\": %.6f}",
+               pr.assemble_profiled, pr.assemble_model, pr.assemble - pr.assemble_model);
+         }
+         std::printf("}");
       }
       std::printf(", \"crosscheck\": [");
       for (size_t k = 0; k < crosscheck_records.size(); ++k) std::printf("%s%s", k ? ", " : "", crosscheck_records[k].c_str());

@@ -2,13 +2,15 @@
 restating the reference loops in the same floating-point order:
 
 - barrier_diagonal         PrimalDualInteriorPointProblem.cpp:56-78 (Sigma)
+- assemble_augmented       uno/ingredients/subproblem/Subproblem.cpp:57-70 after COOFormat::reset (COOFormat.hpp:78-89):
+                           the whole augmented COO value array in Uno's insertion order
 - assemble_augmented_rhs   uno/ingredients/subproblem/Subproblem.cpp:80-99
 - assemble_direction       uno/ingredients/inequality_handling_methods/interior_point_methods/
                            PrimalDualInteriorPointProblem.cpp:173-194 (assemble_primal_dual_direction),
                            :262-278 (compute_bound_dual_direction), :281-325 (fraction-to-boundary)
 - symv / quadratic_product uno/linear_algebra/SymmetricMatrix.hpp:100-130 (COO order)
 
-Pinned to the reference itself: tests/golden/ipm_reference_vectors.json holds the outputs of those very
+Pinned to the reference itself: tests/golden/ipm_reference_vectors.json and augmented_reference_vectors.json hold the outputs of those very
 reference functions (compiled from /root/reference, tests/golden/make_ipm_fixtures.sh) on seeded inputs, and
 tests/test_ipm_vectors.py requires this restatement to reproduce them bit for bit.
 
@@ -32,6 +34,29 @@ def barrier_diagonal(x, lb, ub, zl, zu):
             var.append(i)
             sig.append(d)
     return np.array(var, dtype=np.int64), np.array(sig)
+
+
+def assemble_augmented(reg_size, hess_scale, hess, jac, x, lb, ub, zl, zu):
+    """[0] * reg_size (the regularization diagonal COOFormat::reset re-inserts) ++ hess_scale * hess (the model's
+    Lagrangian Hessian terms, its insertion order; ArrowbandModel inserts sigma * H) ++ Sigma (barrier_diagonal)
+    ++ jac (constraint-major, Subproblem.cpp:64-69).  Elementwise IEEE products, so numpy's vector multiply is the
+    scalar loop's result."""
+    _, sig = barrier_diagonal(x, lb, ub, zl, zu)
+    return np.concatenate([np.zeros(int(reg_size)), float(hess_scale) * np.asarray(hess, dtype=np.float64), sig,
+                           np.asarray(jac, dtype=np.float64)])
+
+
+def barrier_diagonal_vec(x, lb, ub, zl, zu):
+    """barrier_diagonal for large inputs (same operations, vectorised: 0 + a + b with the absent terms skipped)."""
+    x, lb, ub, zl, zu = (np.asarray(a, dtype=np.float64) for a in (x, lb, ub, zl, zu))
+    fl, fu = np.isfinite(lb), np.isfinite(ub)
+    with np.errstate(all="ignore"):
+        a = np.where(fl, zl / (x - lb), 0.0)
+        b = np.where(fu, zu / (x - ub), 0.0)
+    d = np.where(fl, 0.0 + a, 0.0)
+    d = np.where(fu, d + b, d)
+    keep = fl | fu
+    return np.nonzero(keep)[0], d[keep]
 
 
 def assemble_augmented_rhs(grad, cons, y, jac_con, jac_var, jac_val):

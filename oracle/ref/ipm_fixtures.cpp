@@ -31,6 +31,8 @@
 #include "linear_algebra/SparseVector.hpp"
 #include "linear_algebra/Vector.hpp"
 #include "model/Model.hpp"
+#include "model/ModelFactory.hpp"
+#include "models/ArrowbandModel.hpp"
 #include "optimization/Direction.hpp"
 #include "optimization/Iterate.hpp"
 #include "optimization/Multipliers.hpp"
@@ -216,12 +218,96 @@ void one_case(const Options& options, size_t n, size_t m, size_t per_con, double
    print_array("dzu", direction.multipliers.upper_bounds.data(), n, false);
    std::printf("}%s\n", last ? "" : ",");
 }
+// the whole augmented (KKT) value array as the reference assembles it for the synthetic
+// arrowband model through the ipopt chain (ModelFactory::reformulate: slacks + bound relaxation, then
+// PrimalDualInteriorPointProblem), i.e. COOFormat::reset + Subproblem::assemble_augmented_matrix
+// (Subproblem.cpp:57-70) at a seeded interior iterate.  Printed with the device kernel's inputs: the model's
+// Lagrangian Hessian terms at objective multiplier 1 (insertion order) and at `sigma` (a second, direct call of
+// Model::evaluate_lagrangian_hessian), the reformulated problem's Jacobian entries (constraint-major), the
+// relaxed bounds and the iterate.  uno_kkt_assemble_augmented must reproduce `values` bit for bit.
+void augmented_case(const Options& options, size_t N, bool inequality, double sigma, uint64_t seed, bool last) {
+   std::unique_ptr<Model> model = std::make_unique<ArrowbandModel>(N, inequality);
+   model = ModelFactory::reformulate(std::move(model), options);
+   const OptimizationProblem problem(*model);
+   const size_t n = problem.number_variables, m = problem.number_constraints;
+   const InteriorPointParameters parameters{options.get_double("barrier_tau_min"), options.get_double("barrier_k_sigma"),
+      options.get_double("barrier_regularization_exponent"), options.get_double("barrier_small_direction_factor"),
+      options.get_double("barrier_push_variable_to_interior_k1"), options.get_double("barrier_push_variable_to_interior_k2"),
+      options.get_double("barrier_damping_factor")};
+   const PrimalDualInteriorPointProblem barrier_problem(problem, 0.1, parameters);
+   auto hessian_model = HessianModelFactory::create(options);
+   hessian_model->initialize(*model);
+   auto regularization = RegularizationStrategyFactory::create(options);
+   sm_state = seed;
+   Iterate iterate(n, m);
+   Multipliers multipliers(n, m);
+   std::vector<double> lb(n), ub(n);
+   for (size_t i = 0; i < n; ++i) {
+      lb[i] = problem.variable_lower_bound(i);
+      ub[i] = problem.variable_upper_bound(i);
+      const double lo = is_finite(lb[i]) ? lb[i] : -20., hi = is_finite(ub[i]) ? ub[i] : 20.;
+      iterate.primals[i] = lo + (hi - lo) * (0.001 + 0.998 * unif());
+      if (is_finite(lb[i])) multipliers.lower_bounds[i] = std::pow(10., -8. + 16. * unif());
+      if (is_finite(ub[i])) multipliers.upper_bounds[i] = -std::pow(10., -8. + 16. * unif());
+   }
+   for (size_t j = 0; j < m; ++j) multipliers.constraints[j] = 2. * unif() - 1.;
+   const Subproblem subproblem(barrier_problem, iterate, multipliers, *hessian_model, *regularization, INF<double>);
+   RectangularMatrix<double> jacobian(m, n);
+   subproblem.evaluate_jacobian(jacobian);
+   // the reference: the plugin's matrix (PrimalDualInteriorPointMethod.cpp:49-57 sizing), reset, assembled
+   const size_t reg_size = (regularization->performs_primal_regularization() ? problem.get_number_original_variables() : 0) +
+      (regularization->performs_dual_regularization() ? problem.get_equality_constraints().size() : 0);
+   const size_t nnz = barrier_problem.number_hessian_nonzeros(*hessian_model) + barrier_problem.number_jacobian_nonzeros();
+   SparseSymmetricMatrix<COOFormat<size_t, double>> augmented(n + m, nnz, reg_size);
+   augmented.reset();
+   Statistics statistics;
+   subproblem.assemble_augmented_matrix(statistics, augmented, jacobian);
+   std::vector<size_t> rows, cols;
+   std::vector<double> values;
+   for (const auto [r, c, v]: augmented) {
+      rows.push_back(r);
+      cols.push_back(c);
+      values.push_back(v);
+   }
+   // the device kernel's inputs: Hessian terms in the model's insertion order (objective multiplier 1 and sigma)
+   SparseSymmetricMatrix<COOFormat<size_t, double>> h1(n, problem.number_hessian_nonzeros(*hessian_model), 0);
+   SparseSymmetricMatrix<COOFormat<size_t, double>> hs(n, problem.number_hessian_nonzeros(*hessian_model), 0);
+   model->evaluate_lagrangian_hessian(iterate.primals, 1., multipliers.constraints, h1);
+   model->evaluate_lagrangian_hessian(iterate.primals, sigma, multipliers.constraints, hs);
+   std::vector<double> hess1, hess_sigma, jac;
+   for (const auto [r, c, v]: h1) { (void)r; (void)c; hess1.push_back(v); }
+   for (const auto [r, c, v]: hs) { (void)r; (void)c; hess_sigma.push_back(v); }
+   for (size_t j = 0; j < m; ++j) {
+      for (const auto [var, d]: jacobian[j]) { (void)var; jac.push_back(d); }
+   }
+   std::printf("{\"model\": \"%s\", \"N\": %zu, \"n\": %zu, \"m\": %zu, \"reg_size\": %zu, \"sigma\": %.17g, \"seed\": %llu, ",
+      inequality ? "arrowband_ineq" : "arrowband", N, n, m, reg_size, sigma, (unsigned long long)seed);
+   print_array("lb", lb.data(), n);
+   print_array("ub", ub.data(), n);
+   print_array("x", iterate.primals.data(), n);
+   print_array("zl", multipliers.lower_bounds.data(), n);
+   print_array("zu", multipliers.upper_bounds.data(), n);
+   print_array("hess", hess1.data(), hess1.size());
+   print_array("hess_sigma", hess_sigma.data(), hess_sigma.size());
+   print_array("jac", jac.data(), jac.size());
+   print_index("rows", rows);
+   print_index("cols", cols);
+   print_array("values", values.data(), values.size(), false);
+   std::printf("}%s\n", last ? "" : ",");
+}
 } // namespace
 
-int main() {
+int main(int argc, char* argv[]) {
    Options options = DefaultOptions::load();
    options.overwrite_with(DefaultOptions::determine_solvers());
    options.overwrite_with(Presets::get_preset_options(std::optional<std::string>("ipopt")));
+   if (argc > 1 && std::string(argv[1]) == "augmented") {
+      std::printf("[\n");
+      augmented_case(options, 160, false, 0.37, 0xA55E3B1Eull, false);
+      augmented_case(options, 200, true, 1e-3, 0xA55E3B1Full, true);
+      std::printf("]\n");
+      return 0;
+   }
    std::printf("[\n");
    // (n, m, Jacobian entries per constraint, barrier parameter): mu below and above 1 - tau_min
    one_case(options, 300, 120, 6, 0.1, 0x1BADB002ull, false);

@@ -7,3 +7,7 @@
 set -euo pipefail
 make -s -C oracle && make -s -j8 -C oracle/ref fixtures
 oracle/_ref/ipm_fixtures > tests/golden/ipm_reference_vectors.json
+# the reference's own augmented-matrix assembly (COOFormat::reset + Subproblem::
+# assemble_augmented_matrix through the ipopt reformulation chain) for the arrowband model, with the inputs of
+# the device assembly (uno_kkt_assemble_augmented); tests/test_ipm_vectors.py compares bit for bit
+oracle/_ref/ipm_fixtures augmented > tests/golden/augmented_reference_vectors.json

@@ -297,6 +297,46 @@ def test_staged_values_match_host_upload(uno_amd):
     np.testing.assert_array_equal(g.solve(b), host.solve(b))
 
 
+def test_staged_then_device_edit_ordered(uno_amd):
+    """Staged chunks and device-side value edits take effect in call order: chunks of a new set
+    of values are staged (asynchronously, page-locked source), then uno_kkt_fill_values / uno_kkt_set_values
+    edit the regularization prefix on the device before the factorization -- the edit wins over the staged
+    chunk of the same positions, as a sequential copy would have it.  Inputs converted on the fly (float32,
+    strided) stay referenced until the factorization is queried."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(20000, SEEDS["C2"])
+    nnz = len(v)
+    g = HipKKT(0, pin_host_values=1)
+    g.analyze(n, r, c)
+    g.factorize(v)
+    g.inertia()
+    ref = HipKKT(0)
+    ref.analyze(n, r, c)
+    for rep, dw in enumerate((1e-4, 3e-2)):
+        v2 = np.array(v) * (1.0 + 0.25 * rep)
+        vals = v2.copy()
+        bounds = list(range(0, nnz, 1 << 16)) + [nnz]
+        for lo, hi in zip(bounds[:-1], bounds[1:]):
+            g.stage_values(vals, lo, hi - lo)
+        g.fill_values(0, nv, dw)
+        g.set_values(np.arange(nv, n, dtype=np.int64), np.full(n - nv, -1e-8))
+        g.factorize()
+        expect = v2.copy()
+        expect[:nv] = dw
+        expect[nv:n] = -1e-8
+        ref.factorize(expect)
+        assert g.inertia() == ref.inertia()
+        np.testing.assert_array_equal(g.solve(b), ref.solve(b))
+    # a float32 source: every chunk is a converted temporary, kept alive by the wrapper until inertia()
+    v32 = (np.array(v) * 0.5).astype(np.float32)
+    g.stage_values(v32, 0, nnz // 2)
+    g.stage_values(v32, nnz // 2, nnz - nnz // 2)
+    g.factorize()
+    ref.factorize(v32.astype(np.float64))
+    assert g.inertia() == ref.inertia()
+    np.testing.assert_array_equal(g.solve(b), ref.solve(b))
+
+
 def test_empty_and_tiny(uno_amd):
     from uno_amd import HipKKT
     g = HipKKT()

@@ -287,3 +287,115 @@ def test_device_reproduces_reference_vectors(k):
     torch.cuda.synchronize()
     for got, key in zip(out, ("dx", "dy", "dzl", "dzu")):
         np.testing.assert_array_equal(got.cpu().numpy(), c[key], err_msg=key)
+
+
+# ---- the augmented (KKT) value array, SURVEY.md 8(f)2 (tests/golden/augmented_reference_vectors.json: the
+# reference's COOFormat::reset + Subproblem::assemble_augmented_matrix for the arrowband model through the ipopt
+# reformulation chain, with the inputs of the device assembly; tests/golden/make_ipm_fixtures.sh) ----
+def _aug_cases():
+    import json
+    raw = json.load(open(os.path.join(ROOT, "tests", "golden", "augmented_reference_vectors.json")))
+    out = []
+    for c in raw:
+        d = dict(c)
+        for k in ("lb", "ub", "x", "zl", "zu", "hess", "hess_sigma", "jac", "values"):
+            d[k] = np.array([float(v) for v in c[k]])
+        for k in ("rows", "cols"):
+            d[k] = np.array(c[k], dtype=np.int64)
+        out.append(d)
+    return out
+
+
+AUG_CASES = _aug_cases()
+
+
+@pytest.mark.parametrize("k", range(len(AUG_CASES)))
+def test_oracle_reproduces_reference_augmented_matrix(k):
+    """oracle/ipm_oracle.assemble_augmented on the reference's inputs gives the reference's COO values bit for
+    bit; the Hessian terms at objective multiplier sigma are sigma times those at 1 (ArrowbandModel inserts
+    sigma * H), so hess_scale carries the objective multiplier."""
+    c = AUG_CASES[k]
+    vals = ipm_oracle.assemble_augmented(c["reg_size"], 1.0, c["hess"], c["jac"], c["x"], c["lb"], c["ub"], c["zl"], c["zu"])
+    np.testing.assert_array_equal(vals, c["values"])
+    np.testing.assert_array_equal(c["sigma"] * c["hess"], c["hess_sigma"])
+    var, sig = ipm_oracle.barrier_diagonal_vec(c["x"], c["lb"], c["ub"], c["zl"], c["zu"])
+    np.testing.assert_array_equal(sig, ipm_oracle.barrier_diagonal(c["x"], c["lb"], c["ub"], c["zl"], c["zu"])[1])
+
+
+def test_reference_augmented_pattern_is_the_bench_layout():
+    """The bench / parity generator (uno_amd/csrc/arrowband.c) lays its COO out exactly as the reference assembles
+    the arrowband model's KKT (equality case): same (row, col) sequence, entry for entry."""
+    import uno_amd
+    c = next(c for c in AUG_CASES if c["model"] == "arrowband")
+    n, nv, m, r, cc, _, _ = uno_amd.arrowband(c["N"], uno_amd.SEEDS["C2"])
+    assert (n, nv, m) == (c["n"] + c["m"], c["n"], c["m"])
+    np.testing.assert_array_equal(r, c["rows"])
+    np.testing.assert_array_equal(cc, c["cols"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", range(len(AUG_CASES)))
+def test_device_assembly_reproduces_reference_augmented_matrix(k):
+    """uno_kkt_assemble_augmented (device iterate, multipliers and model terms) writes the reference's
+    augmented COO values bit for bit -- every segment: regularization zeros, sigma * H (the objective multiplier
+    applied on the device), Sigma, J -- then factors them on the device with the same inertia as the host copy."""
+    import torch
+    import uno_amd
+    c = AUG_CASES[k]
+    n, m, N = c["n"], c["m"], c["n"] + c["m"]
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    g = uno_amd.HipKKT(0)
+    g.analyze(N, c["rows"], c["cols"])
+    assert g.barrier_setup(c["lb"], c["ub"]) == n
+    g.augmented_setup(c["reg_size"], len(c["hess"]), len(c["jac"]))
+    with pytest.raises(RuntimeError):
+        g.augmented_setup(c["reg_size"], len(c["hess"]) + 1, len(c["jac"]))  # layout != analysed nnz
+    g.augmented_setup(c["reg_size"], len(c["hess"]), len(c["jac"]))
+    H, J, X, ZL, ZU = d(c["hess"]), d(c["jac"]), d(c["x"]), d(c["zl"]), d(c["zu"])
+    vals = torch.full((len(c["values"]),), np.nan, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    g.assemble_augmented(1.0, H.data_ptr(), J.data_ptr(), X.data_ptr(), ZL.data_ptr(), ZU.data_ptr(), vals.data_ptr())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(vals.cpu().numpy(), c["values"])
+    g.assemble_augmented(c["sigma"], H.data_ptr(), J.data_ptr(), X.data_ptr(), ZL.data_ptr(), ZU.data_ptr(), vals.data_ptr())
+    torch.cuda.synchronize()
+    out = vals.cpu().numpy()
+    lo = c["reg_size"]
+    np.testing.assert_array_equal(out[lo:lo + len(c["hess"])], c["hess_sigma"])
+    g.assemble_augmented(1.0, H.data_ptr(), J.data_ptr(), X.data_ptr(), ZL.data_ptr(), ZU.data_ptr(), vals.data_ptr())
+    g.factorize(device_ptr=vals.data_ptr())
+    host = uno_amd.HipKKT(0)
+    host.analyze(N, c["rows"], c["cols"])
+    host.factorize(c["values"])
+    assert g.inertia() == host.inertia()
+
+
+@pytest.mark.gpu
+def test_device_assembly_full_size_c3():
+    """configs[2] size (KKT dimension 1e6, 2e7 values): the device assembly equals the oracle restatement bit for
+    bit on the arrowband layout (Hessian band and Jacobian from the C3 generator, a random interior iterate with
+    the late-IPM multiplier spread)."""
+    import torch
+    import uno_amd
+    N = 1_000_000
+    n, nv, m, r, cc, v, _ = uno_amd.arrowband(N, uno_amd.SEEDS["C3"])
+    nh = sum(min(j, 12) + 1 for j in range(nv))
+    hess, jac = v[n:n + nh], v[n + nh + nv:]
+    rng = np.random.default_rng(3)
+    lb, ub = np.full(nv, -10.0000001), np.full(nv, 10.0000001)
+    x = rng.uniform(-9.9, 9.9, nv)
+    zl = 10.0 ** rng.uniform(-8, 8, nv)
+    zu = -(10.0 ** rng.uniform(-8, 8, nv))
+    g = uno_amd.HipKKT(0)
+    g.analyze(n, r, cc)
+    assert g.barrier_setup(lb, ub) == nv
+    g.augmented_setup(n, nh, len(jac))
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    H, J, X, ZL, ZU = d(hess), d(jac), d(x), d(zl), d(zu)
+    vals = torch.empty(len(v), dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    g.assemble_augmented(1.0, H.data_ptr(), J.data_ptr(), X.data_ptr(), ZL.data_ptr(), ZU.data_ptr(), vals.data_ptr())
+    torch.cuda.synchronize()
+    ref = ipm_oracle.assemble_augmented(n, 1.0, hess, jac, x, lb, ub, zl, zu)
+    got = vals.cpu().numpy()
+    assert got.view(np.uint64).tobytes() == ref.view(np.uint64).tobytes()

@@ -30,8 +30,10 @@ def _driver_present(request):
 
 def drive(args, timeout, env=None):
     """Run the drop-in driver; its last JSON line, or a failure carrying its exit status and stderr."""
-    out = subprocess.run([DRIVER] + args + ["logger=SILENT"], capture_output=True, text=True, timeout=timeout,
-                         env=None if env is None else dict(os.environ, **env))
+    # every drop-in run checks each value-only insert after the analysis against the frozen pattern
+    # (StagedCOOMatrix::insert, UNO_HIPLDL_CHECK_PATTERN): a changed assembly order fails instead of mis-placing values
+    env = dict(os.environ, UNO_HIPLDL_CHECK_PATTERN="1", **(env or {}))
+    out = subprocess.run([DRIVER] + args + ["logger=SILENT"], capture_output=True, text=True, timeout=timeout, env=env)
     lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
     assert lines, f"driver {args} exited {out.returncode} without a result:\n{out.stderr[-3000:]}"
     return json.loads(lines[-1])

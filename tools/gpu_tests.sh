@@ -1,5 +1,5 @@
 #!/bin/bash
-# GPU tests with a heartbeat (the drop-in runs print nothing for minutes): bash tools/r04_tests.sh TAG [pytest args]
+# GPU tests with a heartbeat (the drop-in runs print nothing for minutes): bash tools/gpu_tests.sh TAG [pytest args]
 T=${1:-tests}; shift
 mkdir -p gpurun_out/$T
 ( while true; do date >> gpurun_out/$T/heartbeat.log; sleep 30; done ) &

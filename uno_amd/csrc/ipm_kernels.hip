@@ -241,6 +241,45 @@ __global__ void k_barrier(const int32_t* __restrict__ var, const int8_t* __restr
     }
 }
 
+// The whole augmented (KKT) value array in Uno's insertion order, Subproblem::assemble_augmented_matrix
+// (Subproblem.cpp:57-70) after COOFormat::reset (COOFormat.hpp:78-89, the regularization diagonal first, zeros):
+//   [0, reg)                 0
+//   [reg, reg + nh)          hscale * hess[k]      the Lagrangian Hessian terms as the model inserts them (for a
+//                                                  model with linear constraints: sigma * H, ArrowbandModel.hpp)
+//   [.., + nb)               Sigma_t               PrimalDualInteriorPointProblem.cpp:62-77 (k_barrier's arithmetic)
+//   [.., + nj)               jac[e]                Subproblem.cpp:64-69, constraint-major
+// One streaming pass (every value written once, coalesced; the segments meet in at most 3 waves), the same IEEE
+// operations in the same order as the host code, so bit-identical to it.
+__global__ void k_assemble_augmented(AugArgs A) {
+    const int64_t e1 = A.reg, e2 = e1 + A.nh, e3 = e2 + A.nb, total = e3 + A.nj;
+    for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < total; q += (int64_t)gridDim.x * kT) {
+        double v;
+        if (q < e1) {
+            v = 0.0;
+        } else if (q < e2) {
+            v = A.hscale * A.hess[q - e1];
+        } else if (q < e3) {
+            const int64_t t = q - e2;
+            const int32_t i = A.bvar[t];
+            const int8_t w = A.bwhich[t];
+            v = 0.;
+            if (w & 1) v += A.zl[i] / (A.x[i] - A.lb[i]);
+            if (w & 2) v += A.zu[i] / (A.x[i] - A.ub[i]);
+        } else {
+            v = A.jac[q - e3];
+        }
+        A.values[q] = v;
+    }
+}
+
+hipError_t launch_assemble_augmented(const AugArgs& A, hipStream_t s) {
+    const int64_t total = A.reg + A.nh + A.nb + A.nj;
+    if (total <= 0) return hipSuccess;
+    // grid-stride over at most 8192 blocks of 256 threads (32 blocks per CU)
+    hipLaunchKernelGGL(k_assemble_augmented, dim3(grid_of(total)), dim3(kT), 0, s, A);
+    return hipGetLastError();
+}
+
 hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double* lb, const double* ub, const double* x,
                           const double* zl, const double* zu, int64_t count, double* values, hipStream_t s) {
     if (count <= 0) return hipSuccess;

@@ -47,6 +47,23 @@ struct SymvArgs {
 constexpr int kSymvChunk = 4096;
 constexpr int kSumParts = 1024;  // quadratic_product: block partials of the deterministic two-pass sum
 
+// Subproblem::assemble_augmented_matrix on the device (ipm_kernels.hip k_assemble_augmented)
+struct AugArgs {
+    int64_t reg, nh, nb, nj;    // segment lengths: regularization diagonal, Hessian terms, barrier terms, Jacobian
+    double hscale;              // objective multiplier applied to the Hessian terms
+    const double* hess;         // nh Hessian terms (the model's insertion order)
+    const double* jac;          // nj Jacobian entries (constraint-major)
+    const int32_t* bvar;        // barrier: bounded variables (ascending), nb
+    const int8_t* bwhich;       //          1: finite lower, 2: finite upper bound
+    const double* lb;
+    const double* ub;
+    const double* x;
+    const double* zl;
+    const double* zu;
+    double* values;             // reg + nh + nb + nj COO values
+};
+hipError_t launch_assemble_augmented(const AugArgs& A, hipStream_t s);
+
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
                       const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s);
 hipError_t launch_direction(const DirArgs& A, hipStream_t s);

@@ -197,7 +197,7 @@ struct uno_kkt {
     int solve_rg_bwd = 0;          // option "solve_rg_bwd": register-resident backward walk (k_solve_bwd_rg; its
                                    // transpose-reduced rectangle sums in another order, so the level schedule follows)
     int rg_grid_f = 0, rg_grid_b = 0;
-    bool rg_fwd_ok = false;        // the walk meets k_solve_fwd_rg's precondition (every front p <= 32, m <= 72)
+    int rg_wpe = 3;                // option "solve_rg_wpe": waves per SIMD of the walk kernels' register budget (3 or 4)
     bool new_bwd = false;          // option solve_rg: the backward of one-wave fronts runs the register kernels' arithmetic
                                    // in both schedules (k_solve_bwd_rg / k_solve_bwd_w2)
     int df_win = 0, df_win_opt = 0; // LDS panel window of the dataflow solve (option solve_window, 0 = auto)
@@ -249,6 +249,7 @@ struct uno_kkt {
     DBuf<int8_t> bar_which;               // 1: finite lower, 2: finite upper bound
     DBuf<double> bar_lb, bar_ub;
     int64_t bar_n = -1;
+    int64_t aug_reg = -1, aug_nh = 0, aug_nj = 0;  // uno_kkt_augmented_setup
     DBuf<int32_t> jv_ent, j_con;
     DBuf<unsigned long long> alpha;
     DBuf<double> symv_tmp, symv_part, dot_d;
@@ -289,6 +290,29 @@ namespace {
 int set_err(uno_kkt_t h, int code, const std::string& msg) {
     if (h) h->err = msg;
     return code;
+}
+
+// hipHostUnregister of the caller's page-locked buffer (option pin_host_values) waits for every copy that
+// may still read it: the staged chunks on the upload stream and the factorize / factorize_update copies on
+// the solver's stream (a copy from page-locked memory is a DMA that reads the buffer until it completes)
+void unpin_host_buffer(uno_kkt_t h) {
+    if (!h->pinned_ptr) return;
+    if (h->upload) (void)hipStreamSynchronize(h->upload);
+    if (h->stream) (void)hipStreamSynchronize(h->stream);
+    (void)hipHostUnregister(const_cast<double*>(h->pinned_ptr));
+    (void)hipGetLastError();
+    h->pinned_ptr = nullptr;
+    h->pinned_bytes = 0;
+}
+
+// value edits on the solver's stream (set_values, fill_values, factorize_update) come after the chunks staged
+// so far (uno_kkt_stage_values): the stream waits for the upload stream's last chunk, so a staged chunk of the
+// same positions can never land after the edit (calls take effect in call order)
+hipError_t order_after_staged(uno_kkt_t h) {
+    if (!h->staged_pending) return hipSuccess;
+    hipError_t e = hipEventRecord(h->ev_upload, h->upload);
+    if (e != hipSuccess) return e;
+    return hipStreamWaitEvent(h->stream, h->ev_upload, 0);
 }
 
 #define HIPCHK(h, expr)                                                                              \
@@ -925,7 +949,7 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
 void set_rg_grids(uno_kkt_t h) {
     h->ov_grid = std::min(h->ov_nf, 32);
     for (int d = 0; d < 2; ++d) {
-        const int resident = solve_rg_grid(d == 0, 1 << 30);
+        const int resident = solve_rg_grid(d == 0, 1 << 30, h->rg_wpe);
         int g = std::min(resident, h->rg_nf + h->ov_grid);
         if (resident <= h->ov_grid || (h->rg_nf > 0 && g - h->ov_grid < 1)) g = 0;  // no room: df kernels
         (d == 0 ? h->rg_grid_f : h->rg_grid_b) = g;
@@ -947,7 +971,9 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     for (int32_t f : S.level_fronts)
         if (!dist || h->dist.part.owner[f] == h->rank) walk.push_back(f);
     if (walk.empty()) return hipSuccess;
-    int max_sz = 0, mmax = 0, pmax = 0;
+    // every front of the walk is one-wave eligible; inside it, fronts beyond the register class (p <= 32,
+    // m <= 72) go to the register kernels' second walk (ov_desc, LDS-panel path) -- the split below
+    int max_sz = 0, mmax = 0;
     for (int32_t f : walk) {
         const int m = S.f_m[f], p = S.f_p[f];
         if (p > 64 || m > kMaxLdsFront) {  // a front needs the 256-thread kernels
@@ -956,9 +982,7 @@ hipError_t setup_dataflow(uno_kkt_t h) {
         }
         max_sz = std::max(max_sz, p * m - p * (p - 1) / 2);
         mmax = std::max(mmax, m);
-        pmax = std::max(pmax, p);
     }
-    h->rg_fwd_ok = true;  // fronts beyond the register class take the kernels' LDS-panel path
     // panel window: sized so that 16 one-wave blocks (4 per SIMD, the register limit of the dataflow
     // kernels) fit the 160 KB LDS of a CU; larger panels are processed in column windows
     const int rows_lds = ((mmax + 1) & ~1) + (mmax + 1) / 2;
@@ -1550,7 +1574,7 @@ void uno_kkt_destroy(uno_kkt_t h) {
     for (auto e : h->ev_pool) hipEventDestroy(e);
     if (h->h_counters) hipHostFree(h->h_counters);
     if (h->h_big) hipHostFree(h->h_big);
-    if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
+    unpin_host_buffer(h);
     if (h->stream2) hipStreamSynchronize(h->stream2);
     if (h->ev_scale) hipEventDestroy(h->ev_scale);
     if (h->ev_norm) hipEventDestroy(h->ev_norm);
@@ -1629,7 +1653,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
         }
     }
     else if (n == "solve_rg_wpe") {
-        set_solve_rg_wpe((int)value);
+        h->rg_wpe = (int)value == 4 ? 4 : 3;
         if (h->analyzed) set_rg_grids(h);
     }
     else if (n == "dataflow_solve") {
@@ -1651,7 +1675,7 @@ int uno_kkt_analyze(uno_kkt_t h, int64_t n, int64_t nnz, const int64_t* row, con
     h->analyzed = h->factored = h->factor_enqueued = false;
     h->values_ptr = nullptr;
     h->merges_total = 0;
-    if (h->pinned_ptr) { hipHostUnregister(const_cast<double*>(h->pinned_ptr)); h->pinned_ptr = nullptr; }
+    unpin_host_buffer(h);
     auto t0 = std::chrono::steady_clock::now();
     std::string msg = ukkt::analyze(n, nnz, row, col, h->aopt, h->P, h->S);
     if (!msg.empty()) return set_err(h, UNO_KKT_ERR_ARG, msg);
@@ -1720,6 +1744,7 @@ int uno_kkt_set_values(uno_kkt_t h, const int64_t* positions, const double* v, i
     }
     h->packed_valid = false;
     if (count == 0) return UNO_KKT_OK;
+    HIPCHK(h, order_after_staged(h));
     // a position listed twice keeps its LAST value (the sequential-copy semantics): duplicates are resolved
     // here, so the parallel scatter below writes every position once
     std::vector<int64_t> order((size_t)count);
@@ -1759,7 +1784,7 @@ static void pin_host_buffer(uno_kkt_t h, const double* values) {
     const int64_t nnz = h->S.nnz;
     if (!h->pin_host || nnz <= 0) return;
     if (values == h->pinned_ptr && h->pinned_bytes == (size_t)nnz * sizeof(double)) return;
-    if (h->pinned_ptr) hipHostUnregister(const_cast<double*>(h->pinned_ptr));
+    unpin_host_buffer(h);
     h->pinned_bytes = (size_t)nnz * sizeof(double);
     h->pinned_ptr = hipHostRegister(const_cast<double*>(values), h->pinned_bytes, hipHostRegisterDefault) == hipSuccess
                         ? values : nullptr;
@@ -1779,6 +1804,7 @@ int uno_kkt_fill_values(uno_kkt_t h, int64_t first, int64_t count, double value)
         if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
     }
     h->packed_valid = false;
+    HIPCHK(h, order_after_staged(h));
     int grid = (int)std::min<int64_t>((count + 255) / 256, 4096);
     hipLaunchKernelGGL(k_fill, dim3(grid), dim3(256), 0, h->stream, const_cast<double*>(h->values_ptr) + first, count, value);
     HIPCHK(h, hipGetLastError());
@@ -1795,6 +1821,7 @@ int uno_kkt_factorize_update(uno_kkt_t h, const double* values, int64_t first, i
         const int rc = finish_factorization(h);
         if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
     }
+    HIPCHK(h, order_after_staged(h));
     if (count > 0)
         HIPCHK(h, hipMemcpyAsync(h->values.p + first, values + first, count * sizeof(double), hipMemcpyHostToDevice, h->stream));
     return uno_kkt_factorize(h, nullptr, 0);
@@ -1907,7 +1934,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
     DfArgs Df;
     auto walk = [&](bool forward) -> hipError_t {
         const int g = forward ? h->rg_grid_f : h->rg_grid_b;
-        if (h->rg_fwd_ok && (forward ? h->solve_rg != 0 : h->new_bwd) && g > 0) return launch_solve_rg(A, Df, g, forward, s);
+        if ((forward ? h->solve_rg != 0 : h->new_bwd) && g > 0) return launch_solve_rg(A, Df, g, forward, h->rg_wpe, s);
         return launch_solve_df(A, Df, h->df_grid, h->df_lds, forward, s);
     };
     if (df) {
@@ -2303,6 +2330,39 @@ int uno_kkt_assemble_barrier(uno_kkt_t h, const double* x, const double* zl, con
     if (h->bar_n < 0) return set_err(h, UNO_KKT_ERR_STATE, "assemble_barrier before barrier_setup");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, launch_barrier(h->bar_var.p, h->bar_which.p, h->bar_lb.p, h->bar_ub.p, x, zl, zu, h->bar_n, values, h->stream));
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_augmented_setup(uno_kkt_t h, int64_t reg_size, int64_t nnz_hess, int64_t nnz_jac) {
+    if (!h || reg_size < 0 || nnz_hess < 0 || nnz_jac < 0) return UNO_KKT_ERR_ARG;
+    if (h->bar_n < 0) return set_err(h, UNO_KKT_ERR_STATE, "augmented_setup before barrier_setup");
+    if (h->analyzed && reg_size + nnz_hess + h->bar_n + nnz_jac != h->S.nnz)
+        return set_err(h, UNO_KKT_ERR_ARG, "augmented layout (" + std::to_string(reg_size + nnz_hess + h->bar_n + nnz_jac) +
+                                               " entries) differs from the analysed pattern (" + std::to_string(h->S.nnz) + ")");
+    h->aug_reg = reg_size;
+    h->aug_nh = nnz_hess;
+    h->aug_nj = nnz_jac;
+    return UNO_KKT_OK;
+}
+
+int uno_kkt_assemble_augmented(uno_kkt_t h, double hess_scale, const double* hess, const double* jac, const double* x,
+                               const double* zl, const double* zu, double* values) {
+    if (!h || !values) return UNO_KKT_ERR_ARG;
+    if (h->aug_reg < 0) return set_err(h, UNO_KKT_ERR_STATE, "assemble_augmented before augmented_setup");
+    if ((h->aug_nh > 0 && !hess) || (h->aug_nj > 0 && !jac) || (h->bar_n > 0 && (!x || !zl || !zu)))
+        return UNO_KKT_ERR_ARG;
+    HIPCHK(h, hipSetDevice(h->device));
+    if (h->factor_enqueued && values == h->values_ptr) {  // the queued factorization's redos re-pack from these values
+        const int rc = finish_factorization(h);
+        if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
+    }
+    AugArgs A;
+    A.reg = h->aug_reg; A.nh = h->aug_nh; A.nb = h->bar_n; A.nj = h->aug_nj;
+    A.hscale = hess_scale; A.hess = hess; A.jac = jac;
+    A.bvar = h->bar_var.p; A.bwhich = h->bar_which.p; A.lb = h->bar_lb.p; A.ub = h->bar_ub.p;
+    A.x = x; A.zl = zl; A.zu = zu; A.values = values;
+    HIPCHK(h, launch_assemble_augmented(A, h->stream));
+    if (values == h->values_ptr) h->packed_valid = false;
     return UNO_KKT_OK;
 }
 

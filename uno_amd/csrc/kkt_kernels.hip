@@ -11,6 +11,8 @@
 // with butterfly shuffles, the rank-1/rank-2 Schur updates are spread over a 16x16 thread grid.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
+
 #include <algorithm>
 #include <cfloat>
 #include <cstdio>
@@ -4403,29 +4405,36 @@ hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int ld
 // occupancy query's answer per CU, which can over-report by one), at most the walk length
 static constexpr size_t kRgFwdLds = (192 + (kRgRegion > 8 * 33 ? kRgRegion : 8 * 33)) * sizeof(double);
 static constexpr size_t kRgBwdLds = (32 * 33 > 128 + kRgRegion ? 32 * 33 : 128 + kRgRegion) * sizeof(double);
-static int g_rg_wpe = 3;  // waves per SIMD of the walk kernels' register budget (option "solve_rg_wpe": 3 or 4)
-void set_solve_rg_wpe(int w) { g_rg_wpe = w == 4 ? 4 : 3; }
-int solve_rg_grid(bool forward, int nf) {
-    static int per_cu[4] = {-1, -1, -1, -1}, cus = 0;
-    const int d = (forward ? 0 : 1) + (g_rg_wpe == 4 ? 2 : 0);
-    if (per_cu[d] < 0) {
-        int dev = 0, n = 0;
+// wpe: waves per SIMD of the walk kernels' register budget (per-handle option "solve_rg_wpe": 3 or 4); the
+// occupancy answers are per kernel variant, so the grid always matches the variant launch_solve_rg(wpe) runs
+int solve_rg_grid(bool forward, int nf, int wpe) {
+    // occupancy answers cached per variant; ranks of an in-process group query from their own threads, so the
+    // cache is atomic (every thread computes the same value)
+    static std::atomic<int> per_cu[4] = {{-1}, {-1}, {-1}, {-1}};
+    int cus = 0;
+    const int d = (forward ? 0 : 1) + (wpe == 4 ? 2 : 0);
+    {
+        int dev = 0;
         if (hipGetDevice(&dev) != hipSuccess) return 0;
         if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    }
+    if (per_cu[d].load() < 0) {
+        int n = 0;
         hipError_t e = d == 0   ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_fwd_rg<3>, 64, kRgFwdLds)
                        : d == 1 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_bwd_rg<3>, 64, kRgBwdLds)
                        : d == 2 ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_fwd_rg<4>, 64, kRgFwdLds)
                                 : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, k_solve_bwd_rg<4>, 64, kRgBwdLds);
         if (e != hipSuccess) return 0;
-        per_cu[d] = n - 1;
+        per_cu[d].store(n - 1);
     }
-    if (per_cu[d] < 1) return 0;
-    return (int)std::min<int64_t>((int64_t)per_cu[d] * cus, std::max(nf, 1));
+    const int pc = per_cu[d].load();
+    if (pc < 1) return 0;
+    return (int)std::min<int64_t>((int64_t)pc * cus, std::max(nf, 1));
 }
 
-hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, hipStream_t s) {
+hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, int wpe, hipStream_t s) {
     if (D.nf <= 0 || grid <= 0) return hipSuccess;
-    if (g_rg_wpe == 4) {
+    if (wpe == 4) {
         if (forward) hipLaunchKernelGGL(k_solve_fwd_rg<4>, dim3(grid), dim3(64), kRgFwdLds, s, A, D);
         else hipLaunchKernelGGL(k_solve_bwd_rg<4>, dim3(grid), dim3(64), kRgBwdLds, s, A, D);
     } else {

@@ -276,10 +276,9 @@ hipError_t launch_factor_df(const FactorArgs& A, int mmax, hipStream_t s);
 int solve_df_grid(int lds_doubles, int nf);
 int solve_slack_doubles();
 // register-resident dataflow solve (same DfArgs walk and hand-offs as launch_solve_df; p <= 64, m <= 128)
-int solve_rg_grid(bool forward, int nf);
-void set_solve_rg_wpe(int waves_per_simd);  // 3 or 4 (A/B of the walk kernels' register budget)
+int solve_rg_grid(bool forward, int nf, int waves_per_simd);  // waves_per_simd: 3 or 4 (the kernel variant)
 hipError_t launch_solve_bwd_w2(const SolveArgs& A, const int32_t* fronts, int count, hipStream_t s);
-hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, hipStream_t s);
+hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, int waves_per_simd, hipStream_t s);
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
 // rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch.  Distributed
 // runs: the walk is the rank's own fronts, and the top rows (top_orig, eliminated on rank 0) get the

@@ -48,7 +48,7 @@ EXPORTED_SYMBOLS = [
     "uno_kkt_group_destroy", "uno_kkt_attach_local", "uno_kkt_dist_info", "uno_kkt_rhs_setup",
     "uno_kkt_assemble_rhs", "uno_kkt_assemble_direction", "uno_kkt_symv", "uno_kkt_quadratic_product",
     "uno_kkt_barrier_setup", "uno_kkt_barrier_count", "uno_kkt_assemble_barrier", "uno_kkt_attach_host",
-    "uno_kkt_stage_values",
+    "uno_kkt_stage_values", "uno_kkt_augmented_setup", "uno_kkt_assemble_augmented",
 ]
 
 
@@ -108,6 +108,8 @@ def load_library():
     lib.uno_kkt_barrier_count.argtypes = [vp]
     lib.uno_kkt_barrier_count.restype = ctypes.c_int64
     lib.uno_kkt_assemble_barrier.argtypes = [vp, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.uno_kkt_augmented_setup.argtypes = [vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64]
+    lib.uno_kkt_assemble_augmented.argtypes = [vp, ctypes.c_double, vp, vp, vp, vp, vp, vp]
     lib.uno_kkt_debug_partition.argtypes = [ctypes.c_int64, ctypes.c_int64, _i64p, _i64p, ctypes.c_int,
                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, _i64p]
     lib.uno_kkt_debug_partition.restype = ctypes.c_int64
@@ -194,17 +196,24 @@ class HipKKT:
         """Refactorize after a host edit of positions [first, first+count) of `values` (the array of the
         previous host factorization): only that range is uploaded."""
         v, _ = _f64(values)
-        # the library registers only the buffer of uno_kkt_factorize (kept in self._v_keep); this one is
-        # referenced too, as an asynchronous copy from it may still be in flight
-        self._v_upd = v
+        # the library may page-lock this buffer (pin_host_values) and copies from it asynchronously: it stays
+        # referenced until the factorization has been queried (inertia) -- _in_flight
+        self._in_flight().append(v)
         self._check(self.lib.uno_kkt_factorize_update(self.h, v.ctypes.data_as(ctypes.c_void_p), int(first), int(count)))
 
     def stage_values(self, values, first, count):
         """Asynchronous upload of values[first, first+count) (host array, COO order); the next factorize()
         without arguments factors the staged values (uno_kkt_stage_values)."""
         v, _ = _f64(values)
-        self._v_stage = v  # the copy reads it asynchronously: keep it referenced
+        # every staged chunk's source (a converted temporary for a non-float64 / non-contiguous input) stays
+        # referenced until the factorization that reads it has been queried: the copies are asynchronous
+        self._in_flight().append(v)
         self._check(self.lib.uno_kkt_stage_values(self.h, v.ctypes.data_as(ctypes.c_void_p), int(first), int(count)))
+
+    def _in_flight(self):
+        if not hasattr(self, "_v_in_flight"):
+            self._v_in_flight = []
+        return self._v_in_flight
 
     def fill_values(self, first, count, value):
         self._check(self.lib.uno_kkt_fill_values(self.h, int(first), int(count), float(value)))
@@ -217,6 +226,10 @@ class HipKKT:
     def inertia(self):
         p, q, z = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         self._check(self.lib.uno_kkt_inertia(self.h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(z)))
+        if getattr(self, "_v_in_flight", None):
+            # the factorization is complete: its staged / updated sources were consumed.  A buffer the library
+            # page-locked stays referenced by _v_keep / the list's last entry until another one replaces it
+            self._v_in_flight = self._v_in_flight[-1:]
         return (p.value, q.value, z.value)
 
     def solve(self, rhs):
@@ -248,6 +261,17 @@ class HipKKT:
         """Sigma into the COO values at values_ptr (all DEVICE addresses)."""
         self._check(self.lib.uno_kkt_assemble_barrier(self.h, ctypes.c_void_p(int(x_ptr)), ctypes.c_void_p(int(zl_ptr)),
                                                       ctypes.c_void_p(int(zu_ptr)), ctypes.c_void_p(int(values_ptr))))
+
+    def augmented_setup(self, reg_size, nnz_hess, nnz_jac):
+        """Segment lengths of the augmented COO values (after barrier_setup), uno_kkt_augmented_setup."""
+        self._check(self.lib.uno_kkt_augmented_setup(self.h, int(reg_size), int(nnz_hess), int(nnz_jac)))
+
+    def assemble_augmented(self, hess_scale, hess_ptr, jac_ptr, x_ptr, zl_ptr, zu_ptr, values_ptr):
+        """The whole COO value array in Uno's insertion order on the device (Subproblem::assemble_augmented_matrix):
+        0 on the regularization diagonal, hess_scale * hess, Sigma, jac.  DEVICE addresses (0 for an empty segment)."""
+        P = lambda a: ctypes.c_void_p(int(a)) if a else None
+        self._check(self.lib.uno_kkt_assemble_augmented(self.h, float(hess_scale), P(hess_ptr), P(jac_ptr), P(x_ptr),
+                                                        P(zl_ptr), P(zu_ptr), P(values_ptr)))
 
     def stats(self):
         s = KKTStats()
