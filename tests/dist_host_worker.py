@@ -12,6 +12,10 @@ sys.path.insert(0, os.path.dirname(HERE))
 
 def main():
     rank, world, port, n = (int(a) for a in sys.argv[1:5])
+    # optional 5th argument "rccl_sequence": the options the RCCL transport runs with by default (the dataflow
+    # subtree solve on, dist_dataflow_solve = 1) and the transport calls recorded (comm_trace) for the test to
+    # match sends with receives and collectives across ranks
+    rccl_sequence = len(sys.argv) > 5 and sys.argv[5] == "rccl_sequence"
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     import numpy as np
@@ -22,7 +26,7 @@ def main():
     import uno_amd
     uno_amd.load_library()
     N, nv, m, r, c, v, b = uno_amd.arrowband(n, uno_amd.SEEDS["C5"])
-    g = uno_amd.HipKKT(0)
+    g = uno_amd.HipKKT(0, comm_trace=1, dist_dataflow_solve=1) if rccl_sequence else uno_amd.HipKKT(0)
     g.attach_host(uno_amd.GlooComm(), rank, world)
     g.analyze(N, r, c)
     out = {"rank": rank, "dist": g.dist_info(), "runs": []}
@@ -45,7 +49,9 @@ def main():
                        rel_residual=float(res / (absk * np.abs(x).max() + np.abs(b).max())))
             ref.close()
         out["runs"].append(run)
-    out["stats"] = {k: g.stats()[k] for k in ("factorizations", "solves")}
+    out["stats"] = {k: g.stats()[k] for k in ("factorizations", "solves", "solve_grid", "solve_aborts")}
+    if rccl_sequence:
+        out["comm_trace"] = g.debug_comm_trace()
     g.close()
     dist.barrier()
     dist.destroy_process_group()

@@ -218,6 +218,80 @@ def test_multiprocess_host_transport(world):
     assert r0["stats"]["factorizations"] == 2 and r0["stats"]["solves"] == 2
 
 
+def check_comm_traces(traces):
+    """The transport calls of every rank (option comm_trace) form a consistent RCCL program: the k-th send from
+    rank a to rank b has the size of the k-th receive on b from a, every send / receive sits inside a
+    group_begin / group_end bracket (ncclGroupStart / End), and the collectives (all-reduce count and
+    operation, broadcast size and root) are issued in the same order with the same arguments on every rank."""
+    world = len(traces)
+    coll = []
+    for q, tr in enumerate(traces):
+        depth = 0
+        for op, peer, nbytes, red in tr:
+            if op == "group_begin":
+                depth += 1
+            elif op == "group_end":
+                assert depth > 0, f"rank {q}: group_end without group_begin"
+                depth -= 1
+            elif op in ("send", "recv"):
+                assert depth > 0, f"rank {q}: {op} outside a group"
+                assert 0 <= peer < world and peer != q
+        assert depth == 0
+        coll.append([t for t in tr if t[0] in ("allreduce", "broadcast")])
+    for q in range(1, world):
+        assert coll[q] == coll[0], f"rank {q} collectives differ from rank 0's"
+    for a in range(world):
+        for b in range(world):
+            if a == b:
+                continue
+            sends = [t[2] for t in traces[a] if t[0] == "send" and t[1] == b]
+            recvs = [t[2] for t in traces[b] if t[0] == "recv" and t[1] == a]
+            assert sends == recvs, f"sends {a}->{b} {sends[:8]} vs receives {recvs[:8]}"
+    return sum(len(c) for c in coll[:1]), sum(1 for tr in traces for t in tr if t[0] == "send")
+
+
+@pytest.mark.gpu
+def test_multiprocess_rccl_call_sequence():
+    """VERDICT r4 (multi-GPU): the exact call sequence of the RCCL path -- the options the RCCL transport runs
+    with (one-launch dataflow subtree solves on) and the library's group send / recv and collective calls --
+    driven across two real processes through the host transport over gloo, every call recorded (option
+    comm_trace).  The traces are a consistent RCCL program (matched sizes and order, sends inside groups,
+    identical collectives on both ranks) and the results equal the single-GPU path's."""
+    import json
+    import os
+    import socket
+    import subprocess
+    import sys
+    here = os.path.dirname(os.path.abspath(__file__))
+    world = 2
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = [subprocess.Popen([sys.executable, os.path.join(here, "dist_host_worker.py"), str(q), str(world), str(port),
+                               "60000", "rccl_sequence"], stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+             for q in range(world)]
+    outs = []
+    for p in procs:
+        try:
+            so, se = p.communicate(timeout=240)
+        except subprocess.TimeoutExpired:
+            for pp in procs:
+                pp.kill()
+            raise
+        assert p.returncode == 0, se[-3000:]
+        outs.append(json.loads([l for l in so.splitlines() if l.startswith("{")][-1]))
+    r0 = outs[0]
+    assert r0["dist"]["world"] == world and r0["dist"]["partitioned"] == 1
+    for run_i, run in enumerate(r0["runs"]):
+        assert run["inertia"] == run["ref_inertia"]
+        assert all(o["runs"][run_i]["inertia"] == run["inertia"] for o in outs)
+        assert run["rel_residual"] < RES_TOL
+        assert run["max_rel_diff"] < 1e-9
+    assert all(o["stats"]["solve_grid"] > 0 for o in outs)  # the dataflow subtree solve was armed
+    n_coll, n_send = check_comm_traces([[tuple(t) for t in o["comm_trace"]] for o in outs])
+    assert n_coll > 0 and n_send > 0
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("aborting_rank", [0, 1])
 def test_distributed_abort_on_one_rank(ua, aborting_rank):
@@ -339,3 +413,17 @@ def test_gate_agrees_across_ranks(ua):
         assert out[q][2]["partitioned"] == 0
         assert out[q][0] == ine
         np.testing.assert_array_equal(out[q][1], x)
+
+
+def test_comm_trace_checker_catches_mismatches():
+    """The RCCL-program checker of test_multiprocess_rccl_call_sequence rejects a size mismatch, a send outside
+    a group and diverging collectives (CPU only: synthetic traces)."""
+    good = [[("group_begin", -1, 0, -1), ("send", 1, 64, -1), ("group_end", -1, 0, -1), ("allreduce", -1, 24, 0)],
+            [("group_begin", -1, 0, -1), ("recv", 0, 64, -1), ("group_end", -1, 0, -1), ("allreduce", -1, 24, 0)]]
+    assert check_comm_traces(good) == (1, 1)
+    bad_size = [good[0], [t if t[0] != "recv" else ("recv", 0, 56, -1) for t in good[1]]]
+    bad_group = [[t for t in good[0] if t[0] != "group_begin" and t[0] != "group_end"], good[1]]
+    bad_coll = [good[0], good[1][:-1] + [("allreduce", -1, 24, 1)]]
+    for bad in (bad_size, bad_group, bad_coll):
+        with pytest.raises(AssertionError):
+            check_comm_traces(bad)

@@ -287,4 +287,56 @@ Transport* make_rccl_transport(const unsigned char id[128], int rank, int world,
     return new RcclTransport(c, rank, world);
 }
 
+// ------------------------------------------------------------------------------------------------
+// tracing decorator (option comm_trace)
+// ------------------------------------------------------------------------------------------------
+namespace {
+class TracingTransport final : public Transport {
+public:
+    explicit TracingTransport(Transport* inner) : in_(inner) {}
+    ~TracingTransport() override { delete in_; }
+    int rank() const override { return in_->rank(); }
+    int size() const override { return in_->size(); }
+    std::string describe() const override { return "trace(" + in_->describe() + ")"; }
+    hipError_t group_begin() override { rec(4, -1, 0, -1); return in_->group_begin(); }
+    hipError_t group_end() override { rec(5, -1, 0, -1); return in_->group_end(); }
+    hipError_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+        rec(0, peer, bytes, -1);
+        return in_->send(buf, bytes, peer, s);
+    }
+    hipError_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+        rec(1, peer, bytes, -1);
+        return in_->recv(buf, bytes, peer, s);
+    }
+    hipError_t allreduce(void* buf, size_t count, RedOp op, hipStream_t s) override {
+        rec(2, -1, count * 8, (int)op);
+        return in_->allreduce(buf, count, op, s);
+    }
+    hipError_t broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+        rec(3, root, bytes, -1);
+        return in_->broadcast(buf, bytes, root, s);
+    }
+    std::vector<int64_t> log;
+
+private:
+    void rec(int op, int peer, size_t bytes, int red) {
+        log.push_back(op);
+        log.push_back(peer);
+        log.push_back((int64_t)bytes);
+        log.push_back(red);
+    }
+    Transport* in_;
+};
+}  // namespace
+
+Transport* make_tracing_transport(Transport* inner) { return inner ? new TracingTransport(inner) : nullptr; }
+
+bool comm_trace_records(Transport* t, std::vector<int64_t>& out, bool clear) {
+    auto* tt = dynamic_cast<TracingTransport*>(t);
+    if (!tt) return false;
+    out = tt->log;
+    if (clear) tt->log.clear();
+    return true;
+}
+
 }  // namespace ukkt

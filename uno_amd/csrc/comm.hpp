@@ -18,6 +18,7 @@
 #include <cstddef>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 namespace ukkt {
 
@@ -60,6 +61,15 @@ struct HostComm {
     int (*broadcast)(void* ctx, void* buf, size_t bytes, int root);
 };
 Transport* make_host_transport(const HostComm& cb, int rank, int world);
+
+// Tracing decorator (option comm_trace, tests): forwards every call to `inner` (owned) and records it as
+// (op, peer / root, bytes, reduction op), op: 0 send, 1 recv, 2 allreduce, 3 broadcast, 4 group_begin,
+// 5 group_end.  The library issues the same sequence whatever the transport, so a trace taken through the
+// host or local transport is the sequence the RCCL transport would see (ncclSend / ncclRecv sizes, peers,
+// grouping, collective order).
+Transport* make_tracing_transport(Transport* inner);
+// the records of a tracing transport (empty for any other transport); clear: start a new trace
+bool comm_trace_records(Transport* t, std::vector<int64_t>& out, bool clear);
 
 // RCCL: unique id from rank 0 (NCCL_UNIQUE_ID_BYTES = 128), then every rank attaches with it.
 int rccl_unique_id(unsigned char out[128]);

@@ -273,6 +273,7 @@ struct uno_kkt {
     double dist_efficiency = 0.0; // estimated parallel efficiency of the partition (analysis cost model)
     double dist_min_eff = 0.5;    // option dist_min_efficiency
     int dist_force = 0;           // option dist_force: partition whatever the estimate (tests, experiments)
+    int comm_trace = 0;           // option comm_trace: the transport records its calls (uno_kkt_debug_comm_trace)
     int gather_solution = 1;
     DistState dist;
     uno_kkt_stats_t st{};
@@ -1624,6 +1625,12 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;
     else if (n == "dist_force") h->dist_force = value != 0.0;
+    else if (n == "comm_trace") {  // record the transport calls (tests): wraps the attached transport, if any
+        h->comm_trace = value != 0.0;
+        std::vector<int64_t> dummy;
+        if (h->comm_trace && h->comm && !ukkt::comm_trace_records(h->comm, dummy, false))
+            h->comm = ukkt::make_tracing_transport(h->comm);
+    }
     else if (n == "dataflow_factor") {
         h->dff_enabled = std::max(0, std::min(2, (int)value));
         if (h->analyzed) {
@@ -2467,7 +2474,7 @@ int uno_kkt_comm_unique_id(unsigned char id[128]) {
 
 static int attach(uno_kkt_t h, ukkt::Transport* t) {
     delete h->comm;
-    h->comm = t;
+    h->comm = h->comm_trace ? ukkt::make_tracing_transport(t) : t;
     h->own_device = false;
     h->rank = h->comm_rank = t->rank();
     h->world = h->comm_world = t->size();
@@ -2506,6 +2513,15 @@ int uno_kkt_attach_host(uno_kkt_t h, const uno_kkt_host_comm_t* comm, int rank, 
     ukkt::Transport* t = ukkt::make_host_transport(cb, rank, world);
     if (!t) return set_err(h, UNO_KKT_ERR_ARG, "incomplete host transport or bad rank");
     return attach(h, t);
+}
+
+int64_t uno_kkt_debug_comm_trace(uno_kkt_t h, int64_t* out, int64_t cap, int clear) {
+    if (!h || !h->comm) return -1;
+    std::vector<int64_t> rec;
+    if (!ukkt::comm_trace_records(h->comm, rec, clear != 0)) return -1;
+    const int64_t n = (int64_t)rec.size() / 4;
+    if (out) memcpy(out, rec.data(), sizeof(int64_t) * (size_t)std::min<int64_t>(4 * n, std::max<int64_t>(cap, 0)));
+    return n;
 }
 
 int uno_kkt_dist_info(uno_kkt_t h, uno_kkt_dist_info_t* out) {

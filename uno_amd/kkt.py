@@ -104,6 +104,8 @@ def load_library():
     lib.uno_kkt_dist_info.argtypes = [vp, ctypes.POINTER(KKTDistInfo)]
     lib.uno_kkt_attach_host.argtypes = [vp, ctypes.POINTER(HostCommStruct), ctypes.c_int, ctypes.c_int]
     lib.uno_kkt_debug_scaling.argtypes = [vp, _f64p, _f64p]
+    lib.uno_kkt_debug_comm_trace.argtypes = [vp, _i64p, ctypes.c_int64, ctypes.c_int]
+    lib.uno_kkt_debug_comm_trace.restype = ctypes.c_int64
     lib.uno_kkt_barrier_setup.argtypes = [vp, ctypes.c_int64, _f64p, _f64p]
     lib.uno_kkt_barrier_count.argtypes = [vp]
     lib.uno_kkt_barrier_count.restype = ctypes.c_int64
@@ -241,6 +243,17 @@ class HipKKT:
 
     def solve_device(self, rhs_ptr, x_ptr):
         self._check(self.lib.uno_kkt_solve(self.h, ctypes.c_void_p(int(rhs_ptr)), ctypes.c_void_p(int(x_ptr)), 1))
+
+    def debug_comm_trace(self, clear=False):
+        """Transport calls recorded since the last clear (option comm_trace=1): list of (op, peer, bytes, redop),
+        op in send / recv / allreduce / broadcast / group_begin / group_end; None without a traced transport."""
+        k = int(self.lib.uno_kkt_debug_comm_trace(self.h, None, 0, 0))
+        if k < 0:
+            return None
+        buf = np.zeros(4 * max(k, 1), dtype=np.int64)
+        self.lib.uno_kkt_debug_comm_trace(self.h, buf.ctypes.data_as(_i64p), len(buf), 1 if clear else 0)
+        names = ("send", "recv", "allreduce", "broadcast", "group_begin", "group_end")
+        return [(names[int(buf[4 * i])], int(buf[4 * i + 1]), int(buf[4 * i + 2]), int(buf[4 * i + 3])) for i in range(k)]
 
     def debug_scaling(self):
         """(scale by original index, ||A_pre||_inf) of the last factorization (uno_kkt_debug.h)."""
