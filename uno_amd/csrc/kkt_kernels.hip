@@ -743,6 +743,15 @@ __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x)
     x = umax64(x, dpp64<0x140>(x));  // row_mirror
     return umax64(umax64(readlane64(x, 0), readlane64(x, 16)), umax64(readlane64(x, 32), readlane64(x, 48)));
 }
+__device__ __forceinline__ unsigned long long umin64(unsigned long long a, unsigned long long b) { return a < b ? a : b; }
+// min over the 64 lanes of a wave (every lane must be active; result wave-uniform)
+__device__ __forceinline__ unsigned long long wave_min_u64(unsigned long long x) {
+    x = umin64(x, dpp64<0xB1>(x));
+    x = umin64(x, dpp64<0x4E>(x));
+    x = umin64(x, dpp64<0x141>(x));
+    x = umin64(x, dpp64<0x140>(x));
+    return umin64(umin64(readlane64(x, 0), readlane64(x, 16)), umin64(readlane64(x, 32), readlane64(x, 48)));
+}
 // non-negative doubles compare like their bit patterns
 __device__ __forceinline__ double wave_max_abs(double v) { return as_double(wave_max_u64(as_bits(v))); }
 // an upper bound of wave_max_abs within 2^-20 relative: the maximum of the high words, low word all ones (one
@@ -1120,7 +1129,13 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     bool delays_recorded = false;
     // diagnostics (stamps build path only): shader-clock cycles spent in search / update / rest
     unsigned long long cyc_search = 0, cyc_update = 0, cyc_rest = 0, t_mark = 0;
-    const bool stamping = A.stamps != nullptr;
+    // per-step cycle counters only in a build with UKKT_STEP_STAMPS (a runtime flag costs VALU / SALU in every
+    // pivot step); the phase stamps (assembly / loop / write-out) need no flag here
+#ifdef UKKT_STEP_STAMPS
+    const bool stamping = A.stamps != nullptr && A.stamp_mode != 7;
+#else
+    constexpr bool stamping = false;
+#endif
     int k = 0;
     constexpr bool REG = MR > 0;
     constexpr int RM = MR > 0 ? MR : 1;
@@ -1137,6 +1152,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // one-wave register path: columns whose L was written during the pivot loop (wave-uniform);
     // cleared by any later symmetric interchange (their rows moved: rewritten from LDS at the end)
     unsigned long long fastmask = 0;
+    // one-wave register path: the steps it took (never cleared) and which of them had a negative pivot --
+    // their pivot kinds and inertia counts are written once after the loop instead of per step
+    unsigned long long fastpiv = 0, fastneg = 0;  // columns < 64 (one-wave fronts pivot at most 72 columns)
     bool spilled = false;  // some step ran the LDS path: the LDS front is current after the loop
     double* Lf = A.L + A.L_off[f];
     if constexpr (REG) {
@@ -1166,6 +1184,8 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     // the owners (tx == kk) publish column k (padding rows are 0: stored as is) and test
                     // each candidate: "some u |a_ik| > |a_kk|" is exactly u * max_i |a_ik| > |a_kk| (the
                     // rounding of u * x is monotonic in x); rows <= k of the diagonal block are excluded
+                    // (a max-reduction first would be one product and one compare, but maxnum of loaded values
+                    // costs a canonicalize per element in IEEE mode: 17 dependent DP ops instead of 16 independent)
                     bool bad = false;
                     if (owner) {
 #pragma unroll
@@ -1175,20 +1195,29 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     }
                     need = (__ballot(bad) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
-                    if (!need) {  // 1x1 pivot at k without interchange
-                        minpiv = fmin(minpiv, aak);
+                    if (!need) {  // 1x1 pivot at k without interchange (k < 64: its |a_kk| enters minpiv after the loop)
                         double lv[RM], cv[RM];
 #pragma unroll
                         for (int a = bk; a < RM; ++a) {
                             lv[a] = colw[ty + G * a];
+#ifdef UKKT_DIAG_HALF_LDS
+                            cv[a] = lv[a] * dinv;  // DIAGNOSTIC build only (wrong results): half the LDS operand reads
+#else
                             cv[a] = colw[tx + G * a] * dinv;
+#endif
                         }
                         if (tx <= kk) cv[bk] = 0.0;  // columns <= k keep their values
 #pragma unroll
                         for (int a = bk; a < RM; ++a)
 #pragma unroll
                             for (int b = bk; b <= a; ++b) R[a][b] -= lv[a] * cv[b];
-                        if (tid == 0) { piv[k] = PIV_1X1; if (akk > 0.0) npos++; else nneg++; }
+                        if (k < 64) {  // uniform
+                            fastpiv |= 1ull << k;
+                            fastneg |= (akk > 0.0 ? 0ull : 1ull) << k;
+                        } else {  // columns beyond the masks (fronts of 65..72 columns after delays): per step
+                            minpiv = fmin(minpiv, aak);
+                            if (tid == 0) { piv[k] = PIV_1X1; if (akk > 0.0) npos++; else nneg++; }
+                        }
                         fastmask |= 1ull << k;
                         if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; }
                         k += 1;
@@ -1337,6 +1366,27 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             k += 2;
         }
         if constexpr (REG) reg_load<G, RM>(st, m, R);
+    }
+    if constexpr (REG && W == 1) {
+        // pivot kinds and inertia counts of the register path's 1x1 steps (recorded as bit masks in the loop)
+        if ((fastpiv >> (tid & 63)) & 1) piv[tid & 63] = PIV_1X1;
+        if (tid == 0) {
+            npos += __popcll(fastpiv & ~fastneg);
+            nneg += __popcll(fastneg);
+        }
+        // and the smallest of their |a_kk|: a pivoted column is never updated again, so its diagonal is still the
+        // pivot (R[b][b] of the lanes tx == ty); one wave minimum instead of one fmin per step
+        if (fastpiv) {
+            const int ty = tid / G, tx = tid % G;
+            unsigned long long mn = ~0ull;
+#pragma unroll
+            for (int b = 0; b < RM; ++b) {
+                const int j = tx + G * b;
+                if (ty == tx && j < 64 && ((fastpiv >> j) & 1)) mn = umin64(mn, as_bits(fabs(R[b][b])));
+            }
+            mn = wave_min_u64(mn);
+            if (mn != ~0ull) minpiv = fmin(minpiv, as_double(mn));
+        }
     }
     if constexpr (REG) {
         if (W > 1 || spilled) {  // the write-out below reads the LDS front

@@ -13,7 +13,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libuno_kkt.so")
+# UNO_KKT_LIB: an A/B build of the library elsewhere (experiments only; the tests and the bench use the in-tree one)
+LIB_PATH = os.environ.get("UNO_KKT_LIB") or os.path.join(_HERE, "libuno_kkt.so")
 GEN_PATH = os.path.join(_HERE, "libarrowband.so")
 
 UNO_KKT_OK = 0
