@@ -59,6 +59,13 @@ if os.environ.get("MODE") == "3":
         print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | per step: akk {per[:,0].mean():6.0f} test {per[:,1].mean():6.0f} "
               f"ballot {per[:,2].mean():6.0f} reads {per[:,3].mean():6.0f} fma {per[:,4].mean():6.0f} | loop {loop[s].mean():6.2f} us")
     sys.exit(0)
+if os.environ.get("TAILS"):  # per level: the slowest fronts (the level's tail) -- loop / write maxima and who
+    for lev in range(fl.max() + 1):
+        s = np.nonzero(fl == lev)[0]
+        tot = (st[s, 3] - st[s, 0]) * 10e-3
+        o = s[np.argsort(-tot)[:3]]
+        print(f"level {lev:2d} mean total {tot.mean():6.2f} us, slowest: " + ", ".join(
+            f"f{f} m{fm[f]} p{fp[f]} asm {asm[f]:.1f} loop {loop[f]:.1f} write {wout[f]:.1f}" for f in o))
 for lev in range(fl.max() + 1):
     s = fl == lev
     print(f"level {lev:2d} fronts {s.sum():6d} m {fm[s].mean():6.1f} p {fp[s].mean():5.1f} | assemble {asm[s].mean():7.2f} us "

@@ -70,6 +70,7 @@ struct SolveLaunch {
 // launch plan of a set of fronts: factor launches index fac_fronts, solve launches sol_fronts
 struct Plan {
     DBuf<int32_t> fac_fronts, sol_fronts;
+    std::vector<int32_t> fac_host;  // host copy of fac_fronts (reordered by reorder_slow_first)
     std::vector<Launch> fac;
     std::vector<SolveLaunch> sol;  // ordered by level
 };
@@ -240,6 +241,10 @@ struct uno_kkt {
     uint32_t dff_epoch = 0;
     int64_t dff_aborts = 0;
     DBuf<int32_t> dff_order, dff_nch;
+    std::vector<int32_t> dff_order_host;  // host copy of dff_order (reorder_slow_first)
+    DBuf<int32_t> fslow;                  // per front: steps off the register path in the last factorization
+    int slow_first = 1;                   // option slow_first: reorder the launches after a structure's first factorization
+    bool reorder_due = false;
     DBuf<uint32_t> dff_cnt, dff_ticket;
     // distributed factorization (null comm: one GPU)
     // device-side vector work around the solve
@@ -372,6 +377,7 @@ void flush_timing(uno_kkt_t h) {
 
 int upload_structure(uno_kkt_t h);
 int enqueue_factorization(uno_kkt_t h);
+int reorder_slow_first(uno_kkt_t h);
 int symv_impl(uno_kkt_t h, const double* x, double* y, const double* w, double* dot, bool absval = false);
 
 // Fronts beyond LDS (m > kMaxLdsFront): blocked factorization in HBM scratch (kkt_kernels.hip k_big_*).
@@ -534,7 +540,50 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
     }
     hipError_t e = P.fac_fronts.upload(ffr, h->stream);
     if (e == hipSuccess) e = P.sol_fronts.upload(sfr, h->stream);
+    P.fac_host.swap(ffr);
     return e;
+}
+
+// Slow fronts first (option slow_first, default 1).  The level launches and the dataflow launch dispatch a
+// level's fronts in their list order, and a level ends with its slowest front: a one-wave front whose pivots
+// leave the register path (2x2 pivots, interchanges, null pivots: each such step spills the front to LDS) takes
+// 5-10x the level's mean (C3: 160 us against 33 us at level 1), so a late start of one such front is the
+// level's tail.  After the first factorization of a structure, the per-front count of those steps (fslow)
+// reorders every launch's fronts and the dataflow order within each level, slowest first (ties keep the
+// order by size); the values of later factorizations may move a few pivots, the order stays valid.
+int reorder_slow_first(uno_kkt_t h) {
+    const Symbolic& S = h->S;
+    h->reorder_due = false;
+    if (!h->slow_first || S.nf == 0 || !h->fslow.p) return UNO_KKT_OK;
+    std::vector<int32_t> slow(S.nf);
+    HIPCHK(h, hipMemcpy(slow.data(), h->fslow.p, sizeof(int32_t) * S.nf, hipMemcpyDeviceToHost));
+    int64_t moved = 0;
+    auto by_slow = [&](int32_t a, int32_t b) { return slow[a] > slow[b]; };
+    for (Plan* P : {&h->plan[0], &h->plan[1], &h->dff_plan}) {
+        if (P->fac_host.empty()) continue;
+        bool any = false;
+        for (const Launch& L : P->fac) {
+            if (L.global || L.count < 2) continue;  // large fronts keep their host-driven order
+            auto b = P->fac_host.begin() + L.begin, e = b + L.count;
+            bool has = false;
+            for (auto it = b; it != e && !has; ++it) has = slow[*it] > 0;
+            if (!has) continue;
+            std::stable_sort(b, e, by_slow);
+            any = true;
+            moved++;
+        }
+        if (any) HIPCHK(h, P->fac_fronts.upload(P->fac_host, h->stream));
+    }
+    if (h->dff_level != INT32_MAX && !h->dff_order_host.empty()) {
+        std::stable_sort(h->dff_order_host.begin(), h->dff_order_host.end(), [&](int32_t a, int32_t b) {
+            if (S.f_level[a] != S.f_level[b]) return S.f_level[a] < S.f_level[b];  // children before parents
+            return slow[a] > slow[b];
+        });
+        HIPCHK(h, h->dff_order.upload(h->dff_order_host, h->stream));
+        moved++;
+    }
+    if (h->verbose) fprintf(stderr, "[uno_kkt] slow fronts first: %lld launch lists reordered\n", (long long)moved);
+    return UNO_KKT_OK;
 }
 
 // Rank-local layout of a distributed factorization: subtree partition (identical on every rank),
@@ -876,6 +925,7 @@ int finish_factorization(uno_kkt_t h) {
         return set_err(h, UNO_KKT_ERR_HIP, "internal: inertia does not sum to n");
     }
     h->factored = true;
+    if (h->reorder_due) return reorder_slow_first(h);
     return UNO_KKT_OK;
 }
 
@@ -931,6 +981,7 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
     hipStream_t s = h->stream;
     hipError_t e;
     if ((e = h->dff_order.upload(order, s)) != hipSuccess) return e;
+    h->dff_order_host = order;
     if ((e = h->dff_nch.upload(nch, s)) != hipSuccess) return e;
     if ((e = h->dff_cnt.alloc(S.nf)) != hipSuccess) return e;
     if ((e = hipMemsetAsync(h->dff_cnt.p, 0, sizeof(uint32_t) * S.nf, s)) != hipSuccess) return e;
@@ -1156,6 +1207,8 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->gscratch_off.upload(goff, s));
     HIPCHK(h, h->fstat.alloc(S.nf));
     HIPCHK(h, h->fcnt.alloc(S.nf));
+    HIPCHK(h, h->fslow.alloc(S.nf));
+    h->reorder_due = true;
     HIPCHK(h, h->fmin.alloc(S.nf));
     if (S.nf > 0) HIPCHK(h, hipMemsetAsync(h->fmin.p, 0x7f, sizeof(double) * S.nf, s));  // 1.4e306: above any threshold
     HIPCHK(h, h->perm_d.upload(S.perm, s));
@@ -1395,7 +1448,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.ch_cm = h->ch_cm.p; A.ch_relmap_off = h->ch_relmap_off.p; A.ch_cb_off = h->ch_cb_off.p;
     A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm_p;
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
-    A.counters = h->counters.p; A.fstat = h->fstat.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
+    A.counters = h->counters.p; A.fstat = h->fstat.p; A.fslow = h->fslow.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
     A.big = h->big.p;
     if (h->last_optimistic) A.anorm_bits = nullptr;
@@ -1625,6 +1678,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;
     else if (n == "dist_force") h->dist_force = value != 0.0;
+    else if (n == "slow_first") h->slow_first = value != 0.0;
     else if (n == "comm_trace") {  // record the transport calls (tests): wraps the attached transport, if any
         h->comm_trace = value != 0.0;
         std::vector<int64_t> dummy;

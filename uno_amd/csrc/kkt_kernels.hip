@@ -852,6 +852,118 @@ __device__ PivotDecision search_pivot(const S& st, int m, int k, int p, double u
     return d;
 }
 
+// search_pivot for a front in LDS (PackedStore): the same decisions, with the relaxation ladder's later rungs
+// evaluated candidate-parallel.  The first rung (u) runs exactly as search_pivot (its decision usually comes at
+// the first or second candidate).  When every candidate fails it -- the pivot needs a relaxed threshold --
+// search_pivot would rescan every candidate for each of the five remaining rungs, one after the other (the
+// slowest fronts of a level, in the plugin's relaxed mode); here lane c - c0 evaluates candidate c (chunks of
+// 64) once -- its column maximum g, its 2x2 partner r (the first strict maximum among the fully-summed rows,
+// on the bit patterns), the partner test's maxima gc / gr, with search_pivot's expressions -- and tests it on
+// every rung, and the decision is the first (rung, candidate) that passes: search_pivot's visiting order.
+// The values are those the first rung saw, so minpiv is already complete (no null candidate either: the
+// first rung would have taken it).
+template <class S>
+__device__ PivotDecision search_pivot_par(const S& st, int m, int k, int p, double u, double thres, double& minpiv) {
+    const int lane = threadIdx.x & 63;
+    for (int c = k; c < p; ++c) {  // the first rung (search_pivot with ul = 0)
+        double g = 0.0;
+        unsigned long long best = 0;
+        int bi = 0x7fffffff;
+        for (int i = k + lane; i < m; i += 64) {
+            const double v = i == c ? 0.0 : absA(st, i, c);
+            g = fmax(g, v);
+            const unsigned long long bv = as_bits(v);
+            if (i < p && bv > best) { best = bv; bi = i; }
+        }
+        g = wave_max_abs(g);
+        const double acc = fabs(st.at(c, c));
+        if (fmax(acc, g) <= thres) return PivotDecision{PIV_NULL, c, -1, 0};
+        minpiv = fmin(minpiv, fmax(acc, g));
+        if (acc != 0.0 && acc >= u * g) return PivotDecision{PIV_1X1, c, -1, 0};
+        const unsigned long long mx = wave_max_u64(best);
+        const unsigned long long ik = wave_max_u64(mx != 0 && best == mx ? 0xffffffffull - (unsigned)bi : 0ull);
+        if (mx != 0) {
+            const int r = (int)(0xffffffffull - ik);
+            double gc = 0.0, gr = 0.0;
+            for (int i = k + lane; i < m; i += 64) {
+                const bool skip = i == c || i == r;
+                gc = fmax(gc, skip ? 0.0 : absA(st, i, c));
+                gr = fmax(gr, skip ? 0.0 : absA(st, i, r));
+            }
+            gc = wave_max_abs(gc);
+            gr = wave_max_abs(gr);
+            const double a = st.at(c, c);
+            const double b = r > c ? st.at(r, c) : st.at(c, r);
+            const double e = st.at(r, r);
+            const double det = a * e - b * b;
+            if (det != 0.0) {
+                const double lim = u > 0.0 ? fabs(det) / u : INFINITY;
+                if (fabs(e) * gc + fabs(b) * gr <= lim && fabs(b) * gc + fabs(a) * gr <= lim)
+                    return PivotDecision{PIV_2X2_A, c, r, 0};
+            }
+        }
+    }
+    // rungs 1..5: every candidate at once
+    constexpr int NCH = 2;  // up to 128 candidates (LDS fronts: p <= m <= 128)
+    unsigned ok[NCH];       // bit ul: a 1x1 (low 8 bits) / 2x2 (high 8 bits) pivot passes rung ul
+    int rr[NCH];
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+        const int c = k + 64 * ch + lane;
+        ok[ch] = 0u;
+        rr[ch] = -1;
+        if (k + 64 * ch >= p) continue;  // uniform
+        const int cc = c < p ? c : k;
+        double g = 0.0;
+        unsigned long long best = 0;
+        int bi = 0x7fffffff;
+        for (int i = k; i < m; ++i) {
+            const double v = i == cc ? 0.0 : absA(st, i, cc);
+            g = fmax(g, v);
+            const unsigned long long bv = as_bits(v);
+            if (i < p && bv > best) { best = bv; bi = i; }  // rows ascending: a tie keeps the smaller row
+        }
+        const double acc = fabs(st.at(cc, cc));
+        double gc = 0.0, gr = 0.0, a = 0.0, b = 0.0, e = 0.0, det = 0.0;
+        const bool two = best != 0;
+        if (two) {
+            const int r = bi;
+            rr[ch] = r;
+            for (int i = k; i < m; ++i) {
+                const bool skip = i == cc || i == r;
+                gc = fmax(gc, skip ? 0.0 : absA(st, i, cc));
+                gr = fmax(gr, skip ? 0.0 : absA(st, i, r));
+            }
+            a = st.at(cc, cc);
+            b = r > cc ? st.at(r, cc) : st.at(cc, r);
+            e = st.at(r, r);
+            det = a * e - b * b;
+        }
+#pragma unroll
+        for (int ul = 1; ul < 6; ++ul) {
+            const double uu = ul == 1 ? u * 0.1 : ul == 2 ? u * 0.01 : ul == 3 ? 1e-6 : ul == 4 ? 1e-10 : 0.0;
+            if (acc != 0.0 && acc >= uu * g) ok[ch] |= 1u << ul;
+            if (two && det != 0.0) {
+                const double lim = uu > 0.0 ? fabs(det) / uu : INFINITY;
+                if (fabs(e) * gc + fabs(b) * gr <= lim && fabs(b) * gc + fabs(a) * gr <= lim) ok[ch] |= 0x100u << ul;
+            }
+        }
+        if (c >= p) ok[ch] = 0u;
+    }
+    for (int ul = 1; ul < 6; ++ul) {
+#pragma unroll
+        for (int ch = 0; ch < NCH; ++ch) {
+            const unsigned long long msk = __ballot(((ok[ch] | (ok[ch] >> 8)) >> ul) & 1u);
+            if (msk == 0ull) continue;  // uniform
+            const int w = __ffsll((long long)msk) - 1;
+            const unsigned okw = (unsigned)__builtin_amdgcn_readlane((int)ok[ch], w);
+            const bool is1 = (okw >> ul) & 1u;
+            return PivotDecision{is1 ? PIV_1X1 : PIV_2X2_A, k + 64 * ch + w, is1 ? -1 : __builtin_amdgcn_readlane(rr[ch], w), 1};
+        }
+    }
+    return PivotDecision{PIV_STUCK, k, -1, 0};
+}
+
 // search_pivot for the large fronts in HBM (k_big_panel_reg): the same rule and the same decisions, every
 // thread of the block scanning rows (the one-wave scans cost ~15 us per column at m = 4096)
 template <int T>
@@ -1126,6 +1238,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
     double minpiv = INFINITY;
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
+    int nlds = 0;  // steps through the LDS path (search / interchanges / 2x2 / null)
     bool delays_recorded = false;
     // diagnostics (stamps build path only): shader-clock cycles spent in search / update / rest
     unsigned long long cyc_search = 0, cyc_update = 0, cyc_rest = 0, t_mark = 0;
@@ -1297,13 +1410,18 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             __syncthreads();
         }
         if (stamping) t_mark = __builtin_amdgcn_s_memtime();
+        nlds++;
         if (tid < 64) {
             PivotDecision d;
             if (!REG && quick_1x1(st, m, k, A.u, thres)) {
                 d = PivotDecision{PIV_1X1, k, -1, 0};
                 minpiv = fmin(minpiv, fabs(st.at(k, k)));
             } else {
-                d = search_pivot(st, m, k, p, A.u, thres, minpiv);
+                if constexpr (!kFullStore<S>) {
+                    d = search_pivot_par(st, m, k, p, A.u, thres, minpiv);  // LDS fronts: p - k <= m <= 128
+                } else {
+                    d = search_pivot(st, m, k, p, A.u, thres, minpiv);
+                }
             }
             if (tid == 0) sh->dec = d;
         }
@@ -1564,6 +1682,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     if (sub) A.stamps[8 * f + 7] = __builtin_amdgcn_s_memrealtime();
     if (tid == 0) {
         A.fstat[f] = (int32_t)((nstuck > 0xffff ? 0xffff : nstuck) | ((nrel > 0x7fff ? 0x7fff : nrel) << 16));
+        if (A.fslow) A.fslow[f] = nlds;
         // per-front record instead of global atomics: thousands of fronts finishing together would
         // serialize on the counters' cache line and stall every access routed to that L2 channel
         A.fcnt[f] = (unsigned long long)npos | (unsigned long long)nneg << 16 | (unsigned long long)nzero << 32 |

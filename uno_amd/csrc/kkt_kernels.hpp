@@ -64,6 +64,8 @@ struct FactorArgs {
     int8_t* piv;                // pivot kinds (same layout as rows)
     unsigned long long* counters;  // pos, neg, zero, 2x2, relaxed, stuck, delayed
     int32_t* fstat;             // per front: stuck pivots (low 16 bits) | relaxed pivots (high 16 bits)
+    int32_t* fslow = nullptr;   // per front: pivot steps that left the register path (LDS search / interchange /
+                                // 2x2 / null): the host launches such fronts first in their level (no level tail)
     unsigned long long* fcnt;   // per front: npos | nneg << 16 | nzero << 32 | n2x2 << 48 (summed by launch_count)
     double* fmin;               // per front: smallest pivot magnitude accepted as non-null (min by launch_count)
     const int32_t* fparent;     // assembly-tree parent (-1 = root)
