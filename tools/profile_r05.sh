@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round-4 evidence of the final tree (C3 unless noted), into gpurun_out/r04f: bench line (CPU baseline +
+# Round-5 evidence of the final tree (C3 unless noted), into gpurun_out/r05f: bench line (CPU baseline +
 # shipped-mode line), rocprofv3 kernel-trace stats, one-step timeline, FETCH_SIZE / WRITE_SIZE passes
 # (steady-state factorizations -> pmc_traffic.json), two SQ counter passes, the same-size N=1 point of the
-# distributed curve and the IPM-sequence leg.  Large fronts: tools/r04_big.sh.
+# distributed curve and the IPM-sequence leg.  Large fronts: tools/bigfront_bench.py.
 set -e
 export TMPDIR=/tmp
-R=gpurun_out/r04f
+R=gpurun_out/r05f
 mkdir -p $R
 ( while true; do date >> gpurun_out/heartbeat.log; sleep 30; done ) &
 HB=$!; trap "kill $HB" EXIT
