@@ -371,6 +371,10 @@ def main():
     if world == 1 and not args.no_shipped and not args.profile_only:
         ks = uno_amd.HipKKT(local, delay_relaxed=0)
         ks.set_option("dataflow_solve", args.dataflow)
+        for kv in args.opt:  # A/B options apply to this handle too (its delay_relaxed stays the plugin's)
+            k_, v_ = kv.split("=", 1)
+            if k_ != "delay_relaxed":
+                ks.set_option(k_, float(v_))
         ks.analyze(n, rows, cols)
         torch.cuda.synchronize()
         t1 = time.perf_counter()

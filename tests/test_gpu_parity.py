@@ -456,6 +456,28 @@ def test_threshold_relaxation_with_refinement(uno_amd):
     np.testing.assert_allclose(bd.cpu().numpy(), xg, rtol=1e-12, atol=1e-14 * np.abs(xg).max())
 
 
+def test_refinement_residual_over_fronts(uno_amd):
+    """The refinement residual r = A x - b over the fronts' packed slots (launch_resid: per-front LDS partials,
+    then per-row sums in front order; the default) against the row-wise COO symv it replaced (resid_fronts =
+    0): both refined solutions meet the residual bar and agree to rounding; the chunked path of the dense
+    rows (forced here on every row with more than 4 partials) gives the same; a repeated solve is
+    bit-identical (the per-front accumulation is one wave's, the row sums are in a fixed order)."""
+    from uno_amd import arrowband, SEEDS
+    n, nv, m, r, c, v, b = arrowband(10000, SEEDS["C2"])
+    g1, o = both(n, r, c, v, delay_relaxed=0)
+    g0, _ = both(n, r, c, v, delay_relaxed=0, resid_fronts=0)
+    g2, _ = both(n, r, c, v, delay_relaxed=0, resid_long=4)
+    assert g1.stats()["pivots_relaxed"] > 0
+    x1, x0, x2 = g1.solve(b), g0.solve(b), g2.solve(b)
+    for x in (x1, x0, x2):
+        assert rel_residual(n, r, c, v, x, b) < RES_TOL
+    assert g1.stats()["refinements"] == 1 and g0.stats()["refinements"] == 1
+    np.testing.assert_allclose(x1, x0, rtol=1e-9, atol=1e-12 * np.abs(x0).max())
+    np.testing.assert_allclose(x2, x1, rtol=1e-9, atol=1e-12 * np.abs(x1).max())
+    np.testing.assert_array_equal(g1.solve(b), x1)
+    np.testing.assert_array_equal(g2.solve(b), x2)
+
+
 def test_refine_tol_non_finite(uno_amd):
     """Option refine_tol skips the refinement step only when the componentwise backward error of x is
     finite and below the bound: a NaN in the right-hand side makes omega NaN, which must count as

@@ -69,7 +69,7 @@ def pmc_steady(db, out, skip=3):
     c = sqlite3.connect(db)
     rows = c.execute("select dispatch_id, kernel_name, counter_name, value from counters_collection "
                      "order by dispatch_id").fetchall()
-    starts = sorted({d for d, k, _, _ in rows if "k_reset_counters" in k})
+    starts = sorted({d for d, k, _, _ in rows if "k_reset_counters" in k or "k_sweep_front<true, false>" in k})
     import bisect
     res = {"per_run": {}, "factorizations": max(0, len(starts) - skip), "solves": 0,
            "note": f"steady state: factorizations after the first {skip} (k_reset_counters dispatches); KB per "

@@ -9,6 +9,9 @@ N, nv, m, r, c, v, b = uno_amd.arrowband(n, uno_amd.SEEDS["C3"])
 g = uno_amd.HipKKT(0)
 if os.environ.get("LEAF"):
     g.set_option("leaf_size", int(os.environ["LEAF"]))
+for kv in filter(None, os.environ.get("OPTS", "").split(",")):  # e.g. OPTS=delay_relaxed=0 (the plugin's mode)
+    k_, v_ = kv.split("=")
+    g.set_option(k_, float(v_))
 g.analyze(N, r, c)
 g.factorize(v); g.inertia()
 g.set_option("stamps", int(os.environ.get("MODE", "1")))

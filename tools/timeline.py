@@ -11,7 +11,8 @@ cols = [r[1] for r in c.execute("pragma table_info(kernels)").fetchall()]
 s_col = "start" if "start" in cols else [x for x in cols if "start" in x][0]
 e_col = "end" if "end" in cols else [x for x in cols if x.endswith("end")][0]
 rows = c.execute(f"select name, {s_col}, {e_col} from kernels order by {s_col}").fetchall()
-starts = [i for i, r in enumerate(rows) if "k_reset_counters" in r[0]]
+# a factorization's first kernel: k_reset_counters, or the first equilibration sweep that resets the counters
+starts = [i for i, r in enumerate(rows) if "k_reset_counters" in r[0] or "k_sweep_front<true, false>" in r[0]]
 i0 = starts[-back]
 i1 = starts[-back + 1] if back > 1 else len(rows)
 seg = rows[i0:i1]

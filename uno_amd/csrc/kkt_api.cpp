@@ -265,6 +265,14 @@ struct uno_kkt {
                                           // plugin mode: 3.0e-9 before the step, 4.1e-16 after it)
     DBuf<double> atmp;                    // |A| |x| of the backward-error check
     DBuf<unsigned long long> omega_d;
+    int resid_fronts = 1;                 // option: refinement residual over the fronts' slots (launch_resid)
+    int sweep_reset = 1;                  // option: the first sweep resets the counters (no k_reset_counters)
+    int64_t resid_long = kResidShort;     // option (tests): rows with more partials are summed by chunks
+    int rz_state = 0;                     // 0: index not built, 1: built, -1: not applicable (old symv)
+    DBuf<int32_t> rz_ptr, rz_pos, rz_long, rz_chunk_off, rz_chunk_row;
+    DBuf<double> rz_part, rz_chunk_part;
+    int32_t rz_n_long = 0;
+    int64_t rz_n_chunks = 0;
     int pin_host = 0;                     // option pin_host_values
     const double* pinned_ptr = nullptr;   // caller buffer registered with hipHostRegister
     size_t pinned_bytes = 0;
@@ -1209,6 +1217,7 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->fcnt.alloc(S.nf));
     HIPCHK(h, h->fslow.alloc(S.nf));
     h->reorder_due = true;
+    h->rz_state = 0;
     HIPCHK(h, h->fmin.alloc(S.nf));
     if (S.nf > 0) HIPCHK(h, hipMemsetAsync(h->fmin.p, 0x7f, sizeof(double) * S.nf, s));  // 1.4e306: above any threshold
     HIPCHK(h, h->perm_d.upload(S.perm, s));
@@ -1366,7 +1375,9 @@ hipError_t enqueue_xpos(uno_kkt_t h) {
 int enqueue_factorization(uno_kkt_t h) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
-    HIPCHK(h, launch_reset_counters(h->counters.p, s));  // counters, minbits, anorm
+    // counters, minbits, anorm: reset by the first equilibration sweep when it runs (no launch of its own)
+    const bool reset_in_sweep = h->use_front_sweeps && S.nf > 0 && h->sweep_reset;
+    if (!reset_in_sweep) HIPCHK(h, launch_reset_counters(h->counters.p, s));
     if (h->use_front_sweeps) {
         // k_pack runs inside launch_front_sweeps (timed with the scaling)
     } else {
@@ -1409,6 +1420,7 @@ int enqueue_factorization(uno_kkt_t h) {
             W.rows_total = (int64_t)S.rows.size();
             W.flong = h->n_long > 0 ? h->flong.p : nullptr;
             W.rmax_zero = h->rmaxk_clean;
+            W.counters = reset_in_sweep ? h->counters.p : nullptr;
             HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
             h->rmaxk_clean = true;  // k_sweep_final cleared it
             if (h->overlap_norm && !h->exact_next) {
@@ -1663,6 +1675,9 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "delay_relaxed") h->delay_relaxed = value != 0.0;
     else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "refine_tol") h->refine_tol = std::max(0.0, value);
+    else if (n == "sweep_reset") h->sweep_reset = value != 0.0;
+    else if (n == "resid_fronts") { h->resid_fronts = value != 0.0; h->rz_state = 0; }
+    else if (n == "resid_long") { h->resid_long = std::max<int64_t>(1, (int64_t)value); h->rz_state = 0; }
     else if (n == "pin_host_values") h->pin_host = value != 0.0;
     else if (n == "front_sweeps") h->front_sweeps = value != 0.0;
     else if (n == "stamps") h->want_stamps = (int)value;
@@ -1970,7 +1985,10 @@ namespace {
 // One solve with the last factorization, device pointers (b may alias xd: b is read by the first kernel,
 // xd written by the last).  Returns after the stream has drained when the dataflow solve ran (its abort
 // flag is checked in the same call; an aborted solve is redone with the level schedule, allow_df = false).
-int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
+// check = false (refined solves): the dataflow abort flag is not read here; the caller reads it once after
+// the refinement (the flag stays set through the later walks) and redoes the whole solve level by level
+// sub_into (a refinement correction): x = A^-1 b is subtracted from sub_into (xd is scratch then)
+int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true, bool check = true, double* sub_into = nullptr) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
     const bool df = allow_df && h->df_enabled && h->df_grid > 0;
@@ -2091,9 +2109,11 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
             HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, h->dist.n_own, s, h->dist.own_orig.p));
             HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, h->dist.n_top_rows, s, h->dist.top_orig.p));
         } else if (df) {
-            HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, S.n, s));
+            if (sub_into) HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, sub_into, S.n, s, nullptr, true));
+            else HIPCHK(h, launch_xs_out(h->df_xs.p, h->scale.p, h->df_xpos.p, h->df_abort.p, xd, S.n, s));
         } else {
             HIPCHK(h, launch_unscale(h->w.p, h->scale.p, xd, S.n, s));
+            if (sub_into) HIPCHK(h, launch_sub(sub_into, xd, S.n, s));
         }
     }
     if (dist && h->gather_solution) {
@@ -2111,7 +2131,7 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
         if (h->rank == 0)
             HIPCHK(h, launch_scatter(D.xbuf.p, D.all_own_orig.p, xd, D.all_own_off[h->world], s));
     }
-    if (df && !dist) {
+    if (df && !dist && check) {
         // one GPU: k_xs_out itself skips the write of x on an abort (x may alias the rhs); the flag is read
         // in the same call and the solve redone with the level schedule
         HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -2119,9 +2139,94 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true) {
         if (dataflow_aborted(h)) {
             if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: this solve redone level by level\n");
-            return solve_core(h, b, xd, false);
+            return solve_core(h, b, xd, false, true, sub_into);
         }
     }
+    return UNO_KKT_OK;
+}
+
+// The row -> front-row index of launch_resid, built on the first refinement of a structure: the front rows
+// (f, q) that hold a slot of their row (q is one of the slot's two local indices), per row in front order.
+// Not applicable (the COO symv then): fronts with more than kSweepBigSlots slots (one wave would take them
+// alone), fronts beyond the sweeps' LDS, or more front rows than int32 positions.
+int build_resid_index(uno_kkt_t h) {
+    Symbolic& S = h->S;
+    hipStream_t s = h->stream;
+    const int64_t nr = (int64_t)S.rows.size();
+    bool ok = h->resid_fronts != 0 && S.max_m <= kMaxSweepFront && nr < INT32_MAX && S.n < INT32_MAX;
+    for (int64_t f = 0; ok && f < S.nf; ++f) ok = S.f_ent_off[f + 1] - S.f_ent_off[f] <= kSweepBigSlots;
+    if (!ok) {
+        h->rz_state = -1;
+        return UNO_KKT_OK;
+    }
+    std::vector<uint8_t> act((size_t)std::max<int64_t>(nr, 1), 0);
+    for (int64_t f = 0; f < S.nf; ++f) {
+        const int64_t ro = S.f_rows_off[f];
+        for (int64_t e = S.f_ent_off[f]; e < S.f_ent_off[f + 1]; ++e) {
+            act[ro + (S.ent_lpos[e] >> 16)] = 1;
+            act[ro + (S.ent_lpos[e] & 0x7fffu)] = 1;
+        }
+    }
+    std::vector<int32_t> ptr((size_t)S.n + 1, 0);
+    for (int64_t t = 0; t < nr; ++t)
+        if (act[t]) ptr[S.rows[t] + 1]++;
+    for (int64_t i = 0; i < S.n; ++i) ptr[i + 1] += ptr[i];
+    std::vector<int32_t> pos((size_t)std::max<int32_t>(ptr[S.n], 1)), fill(ptr.begin(), ptr.end() - 1);
+    for (int64_t t = 0; t < nr; ++t)  // t ascending = front ascending
+        if (act[t]) pos[fill[S.rows[t]]++] = (int32_t)t;
+    std::vector<int32_t> lr, coff(1, 0), crow;
+    for (int64_t i = 0; i < S.n; ++i) {
+        const int64_t len = ptr[i + 1] - ptr[i];
+        if (len <= std::min<int64_t>(h->resid_long, kResidShort)) continue;
+        const int32_t nc = (int32_t)((len + kResidChunk - 1) / kResidChunk);
+        crow.insert(crow.end(), nc, (int32_t)lr.size());
+        lr.push_back((int32_t)i);
+        coff.push_back(coff.back() + nc);
+    }
+    HIPCHK(h, h->rz_ptr.upload(ptr, s));
+    HIPCHK(h, h->rz_pos.upload(pos, s));
+    HIPCHK(h, h->rz_part.alloc(std::max<int64_t>(nr, 1)));
+    h->rz_n_long = (int32_t)lr.size();
+    h->rz_n_chunks = (int64_t)crow.size();
+    if (!lr.empty()) {
+        HIPCHK(h, h->rz_long.upload(lr, s));
+        HIPCHK(h, h->rz_chunk_off.upload(coff, s));
+        HIPCHK(h, h->rz_chunk_row.upload(crow, s));
+        HIPCHK(h, h->rz_chunk_part.alloc(h->rz_n_chunks));
+    }
+    HIPCHK(h, hipStreamSynchronize(s));  // the host vectors go out of scope
+    h->rz_state = 1;
+    return UNO_KKT_OK;
+}
+
+// r = A x - b (refinement residual): launch_resid over the fronts' slots, or the COO symv (r = -b, r += A x)
+int resid_impl(uno_kkt_t h, const double* x, const double* b, double* r) {
+    Symbolic& S = h->S;
+    hipStream_t s = h->stream;
+    if (h->rz_state == 0) {
+        int rc = build_resid_index(h);
+        if (rc != UNO_KKT_OK) return rc;
+    }
+    if (h->rz_state < 0 || h->resid_fronts == 0) {
+        HIPCHK(h, launch_neg(b, r, S.n, s));
+        return symv_impl(h, x, r, nullptr, nullptr);
+    }
+    if (!h->packed_valid) {
+        HIPCHK(h, launch_pack(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->slot_src.p, 0, S.nu, h->uval.p, s));
+        if (h->slot_src.p) HIPCHK(h, launch_pack_multi(h->values_ptr, h->dup_ptr.p, h->dup_pos.p, h->multi_slots.p, h->n_multi, h->uval.p, s));
+        h->packed_valid = true;
+    }
+    ResidArgs A;
+    A.nf = S.nf; A.n = S.n; A.fm = h->fm.p; A.rows_off = h->rows_off.p; A.rows = h->rows.p; A.ent_off = h->ent_off.p;
+    A.ent_lpos = h->ent_lpos.p; A.uval = h->uval.p; A.x = x; A.b = b; A.part = h->rz_part.p; A.rz_ptr = h->rz_ptr.p;
+    A.rz_pos = h->rz_pos.p; A.r = r; A.max_m = (int)S.max_m;
+    A.short_len = (int32_t)std::min<int64_t>(h->resid_long, kResidShort);
+    if (h->rz_n_long > 0) {
+        A.long_rows = h->rz_long.p; A.n_long = h->rz_n_long; A.chunk_off = h->rz_chunk_off.p;
+        A.n_chunks = h->rz_n_chunks; A.chunk_row = h->rz_chunk_row.p; A.chunk_part = h->rz_chunk_part.p;
+    }
+    TimerScope t(h, KC_SYMV);
+    HIPCHK(h, launch_resid(A, s));
     return UNO_KKT_OK;
 }
 }  // namespace
@@ -2153,30 +2258,45 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         if (S.n > 0) HIPCHK(h, hipMemcpyAsync(h->bvec.p, rhs, S.n * sizeof(double), hipMemcpyDeviceToDevice, s));
         b = h->bvec.p;
     }
-    int rc = solve_core(h, b, xd);
-    if (rc != UNO_KKT_OK) return rc;
-    for (int it = 0; it < refine; ++it) {
-        HIPCHK(h, launch_neg(b, h->rtmp.p, S.n, s));              // r = -b
-        if ((rc = symv_impl(h, xd, h->rtmp.p, nullptr, nullptr)) != UNO_KKT_OK) return rc;  // r += A x
-        if (h->refine_tol > 0.0) {
-            // componentwise backward error omega = max_i |r_i| / (|A| |x| + |b|)_i; the step is skipped when
-            // x already satisfies omega <= refine_tol (one extra |A| |x| product and a scalar read-back)
-            if (h->atmp.n != (size_t)S.n) HIPCHK(h, h->atmp.alloc(std::max<int64_t>(S.n, 1)));
-            if (!h->omega_d.p) HIPCHK(h, h->omega_d.alloc(1));
-            if (S.n > 0) HIPCHK(h, hipMemsetAsync(h->atmp.p, 0, sizeof(double) * S.n, s));
-            if ((rc = symv_impl(h, xd, h->atmp.p, nullptr, nullptr, true)) != UNO_KKT_OK) return rc;
-            HIPCHK(h, launch_backward_error(h->rtmp.p, h->atmp.p, b, S.n, h->omega_d.p, s));
-            unsigned long long bits = 0;
-            HIPCHK(h, hipMemcpyAsync(&bits, h->omega_d.p, sizeof(bits), hipMemcpyDeviceToHost, s));
-            HIPCHK(h, hipStreamSynchronize(s));
-            double omega;
-            memcpy(&omega, &bits, sizeof(omega));
-            h->st.last_backward_error = omega;
-            if (omega <= h->refine_tol) { h->st.refinements_skipped++; break; }
+    // with refinement the dataflow abort flag is read once, after the last correction (one host wait per
+    // solve instead of one per solve_core); an abort redoes the solve and its refinement level by level
+    auto refined_solve = [&](bool allow_df) -> int {
+        int rc = solve_core(h, b, xd, allow_df, refine == 0);
+        if (rc != UNO_KKT_OK) return rc;
+        for (int it = 0; it < refine; ++it) {
+            if ((rc = resid_impl(h, xd, b, h->rtmp.p)) != UNO_KKT_OK) return rc;  // r = A x - b
+            if (h->refine_tol > 0.0) {
+                // componentwise backward error omega = max_i |r_i| / (|A| |x| + |b|)_i; the step is skipped when
+                // x already satisfies omega <= refine_tol (one extra |A| |x| product and a scalar read-back)
+                if (h->atmp.n != (size_t)S.n) HIPCHK(h, h->atmp.alloc(std::max<int64_t>(S.n, 1)));
+                if (!h->omega_d.p) HIPCHK(h, h->omega_d.alloc(1));
+                if (S.n > 0) HIPCHK(h, hipMemsetAsync(h->atmp.p, 0, sizeof(double) * S.n, s));
+                if ((rc = symv_impl(h, xd, h->atmp.p, nullptr, nullptr, true)) != UNO_KKT_OK) return rc;
+                HIPCHK(h, launch_backward_error(h->rtmp.p, h->atmp.p, b, S.n, h->omega_d.p, s));
+                unsigned long long bits = 0;
+                HIPCHK(h, hipMemcpyAsync(&bits, h->omega_d.p, sizeof(bits), hipMemcpyDeviceToHost, s));
+                HIPCHK(h, hipStreamSynchronize(s));
+                double omega;
+                memcpy(&omega, &bits, sizeof(omega));
+                h->st.last_backward_error = omega;
+                if (omega <= h->refine_tol) { h->st.refinements_skipped++; break; }
+            }
+            // x -= A^-1 r (the subtraction fused into the solve's write-out)
+            if ((rc = solve_core(h, h->rtmp.p, h->rtmp.p, allow_df, false, xd)) != UNO_KKT_OK) return rc;
+            h->st.refinements++;
         }
-        if ((rc = solve_core(h, h->rtmp.p, h->rtmp.p)) != UNO_KKT_OK) return rc;          // d = A^-1 r
-        HIPCHK(h, launch_sub(xd, h->rtmp.p, S.n, s));             // x -= d
-        h->st.refinements++;
+        return UNO_KKT_OK;
+    };
+    int rc = refined_solve(true);
+    if (rc != UNO_KKT_OK) return rc;
+    if (refine > 0 && h->df_enabled && h->df_grid > 0) {
+        HIPCHK(h, hipMemcpyAsync(h->h_counters + 10, h->df_abort.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        HIPCHK(h, host_wait_stream(h, s));
+        if (dataflow_aborted(h)) {
+            if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
+            if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: the refined solve redone level by level\n");
+            if ((rc = refined_solve(false)) != UNO_KKT_OK) return rc;
+        }
     }
     h->st.solves++;
     if (!on_device) {

@@ -443,6 +443,15 @@ __global__ __launch_bounds__(256) void k_rowscanR(ScanArgs A) {
     if (lane == 0) rowR_write<MODE>(A, i, acc, si);
 }
 
+template <int CTRL>
+__device__ __forceinline__ unsigned long long dpp64(unsigned long long x) {
+    unsigned lo = (unsigned)x, hi = (unsigned)(x >> 32);
+    lo = (unsigned)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xf, 0xf, false);
+    hi = (unsigned)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xf, 0xf, false);
+    return ((unsigned long long)hi << 32) | lo;
+}
+__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
+
 // ---- single-GPU equilibration on the fronts' slots (SweepArgs) ----
 // Every entry of the lower triangle is one packed slot of exactly one front, and both its rows are in
 // that front's row list, so a row's maximum is the maximum over the fronts holding it of the front's
@@ -500,6 +509,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     unsigned long long* rm = reinterpret_cast<unsigned long long*>(swm + m);  // m: row maxima (bits)
     const int64_t ro = A.rows_off[f];
     int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    if (FIRST && !BIG && A.counters && blockIdx.x == 0 && lane < kCounterSlots) A.counters[lane] = lane == 8 ? ~0ull : 0ull;
     if (!BIG && e1 - e0 > kSweepBigSlots) return;
     if (BIG) {
         const int64_t chunk = ((e1 - e0 + gridDim.y - 1) / gridDim.y + 7) & ~(int64_t)7;
@@ -587,16 +597,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void k
     for (int64_t base = e0;;) {
 #pragma unroll
         for (int u = 0; u < EB; ++u) {
-            if (lp[u] == 0xffffffffu) continue;  // beyond the slot range
-            const int lr = (int)(lp[u] >> 16), lc = (int)(lp[u] & 0x7fffu);
-            double w = fabs(v[u]);
-            if (!FIRST) {
+            // slots are column-major, so runs of lanes share a column: an aligned quad whose four slots are in
+            // one column reduces its maximum across the quad (DPP) and its first lane does the column's
+            // atomic -- a quarter of the same-address LDS atomics (max is order-free: same result)
+            const bool ok = lp[u] != 0xffffffffu;  // beyond the slot range: no atomics
+            const int lr = (int)(lp[u] >> 16), lc = ok ? (int)(lp[u] & 0x7fffu) : -1;
+            double w = ok ? fabs(v[u]) : 0.0;
+            if (!FIRST && ok) {
                 const double sr = sl[lr], sc = sl[lc];
                 w = (lp[u] & 0x8000u) ? sc * w * sr : sr * w * sc;
             }
             const unsigned long long bw = as_bits(w);
-            atomicMax(rm + lr, bw);
-            atomicMax(rm + lc, bw);
+            // every DPP read in all lanes (a short-circuit && would evaluate the last one under a partial EXEC)
+            const int s1 = lc == __builtin_amdgcn_mov_dpp(lc, 0xB1, 0xF, 0xF, false) ? 1 : 0;  // quad_perm [1,0,3,2]
+            const int s2 = lc == __builtin_amdgcn_mov_dpp(lc, 0x4E, 0xF, 0xF, false) ? 1 : 0;  // quad_perm [2,3,0,1]
+            const int s3 = __builtin_amdgcn_mov_dpp(s1, 0x4E, 0xF, 0xF, false);               // the other pair
+            const bool same = (s1 & s2 & s3) != 0;
+            unsigned long long qm = umax64(bw, dpp64<0xB1>(bw));
+            qm = umax64(qm, dpp64<0x4E>(qm));
+            if (ok) atomicMax(rm + lr, bw);
+            if (same) {
+                if ((lane & 3) == 0 && lc >= 0) atomicMax(rm + lc, qm);
+            } else if (ok) {
+                atomicMax(rm + lc, bw);
+            }
         }
         base += (int64_t)EB * NT;
         if (base >= e1) break;  // uniform
@@ -635,15 +659,115 @@ __global__ __launch_bounds__(256) void k_sweep_long_fin(SweepArgs A) {
     for (int k = threadIdx.x; k < A.n_long; k += 256) lred[k] = 0ull;
     __syncthreads();
     const int64_t stride = (int64_t)gridDim.x * 256;
-    for (int k = 0; k < A.n_long; ++k) {
-        double mx = 0.0;
-        for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < A.nf; f += stride) mx = fmax(mx, A.part_long[f * A.n_long + k]);
-        for (int off = 32; off > 0; off >>= 1) mx = fmax(mx, __shfl_xor(mx, off));
-        if ((threadIdx.x & 63) == 0 && mx > 0.0) atomicMax(lred + k, as_bits(mx));
+    constexpr int KB = 8;  // long rows per pass: their partial loads in flight together
+    for (int k0 = 0; k0 < A.n_long; k0 += KB) {
+        double mx[KB];
+#pragma unroll
+        for (int u = 0; u < KB; ++u) mx[u] = 0.0;
+        for (int64_t f = (int64_t)blockIdx.x * 256 + threadIdx.x; f < A.nf; f += stride) {
+#pragma unroll
+            for (int u = 0; u < KB; ++u)
+                if (k0 + u < A.n_long) mx[u] = fmax(mx[u], A.part_long[f * A.n_long + k0 + u]);
+        }
+#pragma unroll
+        for (int u = 0; u < KB; ++u) {
+            for (int off = 32; off > 0; off >>= 1) mx[u] = fmax(mx[u], __shfl_xor(mx[u], off));
+            if ((threadIdx.x & 63) == 0 && k0 + u < A.n_long && mx[u] > 0.0) atomicMax(lred + k0 + u, as_bits(mx[u]));
+        }
     }
     __syncthreads();
     for (int k = threadIdx.x; k < A.n_long; k += 256)
         if (lred[k] != 0ull) atomicMax(A.rmax + A.long_orig[k], lred[k]);
+}
+
+// ---- refinement residual over the fronts' slots (ResidArgs) ----
+__global__ __launch_bounds__(64) void k_resid_front(ResidArgs A) {
+    extern __shared__ __attribute__((aligned(16))) double rsm[];
+    const int f = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t e0 = A.ent_off[f], e1 = A.ent_off[f + 1];
+    if (e1 == e0) return;  // no slot: none of its rows has a partial here
+    const int m = A.fm[f];
+    const int64_t ro = A.rows_off[f];
+    double* xl = rsm;      // m: x of the front rows
+    double* yl = rsm + m;  // m: the front's partial A x
+    for (int q = lane; q < m; q += 64) {
+        xl[q] = A.x[A.rows[ro + q]];
+        yl[q] = 0.0;
+    }
+    __syncthreads();
+    constexpr int EB = 8;  // load u of lane l reads slot base + 64 u + l (coalesced), as the sweeps
+    for (int64_t base = e0; base < e1; base += EB * 64) {
+        uint32_t lp[EB];
+        double v[EB];
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            const int64_t e = base + (int64_t)u * 64 + lane;
+            const bool ok = e < e1;
+            lp[u] = ok ? A.ent_lpos[e] : 0xffffffffu;
+            v[u] = ok ? A.uval[e] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < EB; ++u) {
+            if (lp[u] == 0xffffffffu) continue;
+            const int lr = (int)(lp[u] >> 16), lc = (int)(lp[u] & 0x7fffu);
+            atomicAdd(yl + lr, v[u] * xl[lc]);
+            if (lr != lc) atomicAdd(yl + lc, v[u] * xl[lr]);
+        }
+    }
+    __syncthreads();
+    for (int q = lane; q < m; q += 64) A.part[ro + q] = yl[q];
+}
+
+// waves [0, n_chunks): chunk q of the chunked rows (4 partials per lane, fixed tree) -> chunk_part[q]; then
+// 4 lanes per row (up to 8 partials per lane, summed in order, fixed tree) -> r
+__global__ __launch_bounds__(256) void k_resid_rows(ResidArgs A) {
+    const int64_t wave = ((int64_t)blockIdx.x * 256 + threadIdx.x) >> 6;
+    const int lane = threadIdx.x & 63;
+    if (wave < A.n_chunks) {
+        const int k = A.chunk_row[wave];
+        const int32_t i = A.long_rows[k];
+        const int32_t b = A.rz_ptr[i] + (int32_t)(wave - A.chunk_off[k]) * kResidChunk;
+        const int32_t e = min(A.rz_ptr[i + 1], b + kResidChunk);
+        int32_t pos[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const int32_t t = b + u * 64 + lane;
+            pos[u] = t < e ? A.rz_pos[t] : -1;
+        }
+        double acc = 0.0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) acc += pos[u] >= 0 ? A.part[pos[u]] : 0.0;
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off);
+        if (lane == 0) A.chunk_part[wave] = acc;
+        return;
+    }
+    const int64_t g = (((int64_t)blockIdx.x * 256 + threadIdx.x) - A.n_chunks * 64) >> 2;
+    const int q = threadIdx.x & 3;
+    if (g >= A.n) return;
+    const int32_t p0 = A.rz_ptr[g], p1 = A.rz_ptr[g + 1];
+    if (p1 - p0 > A.short_len) return;  // chunked
+    int32_t pos[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+        const int32_t t = p0 + u * 4 + q;
+        pos[u] = t < p1 ? A.rz_pos[t] : -1;
+    }
+    double acc = 0.0;
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc += pos[u] >= 0 ? A.part[pos[u]] : 0.0;
+    acc += __shfl_xor(acc, 2, 4);
+    acc += __shfl_xor(acc, 1, 4);
+    if (q == 0) A.r[g] = acc - A.b[g];
+}
+
+__global__ void k_resid_long_fin(ResidArgs A) {
+    const int k = blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= A.n_long) return;
+    const int32_t i = A.long_rows[k];
+    double acc = 0.0;
+    for (int32_t c = A.chunk_off[k]; c < A.chunk_off[k + 1]; ++c) acc += A.chunk_part[c];
+    A.r[i] = acc - A.b[i];
 }
 
 // after the front sweeps: scale (by original id perm[i]) = sweep_row_scale of new index i over all `iters`
@@ -714,13 +838,6 @@ __device__ __forceinline__ double absA(const S& st, int i, int c) {
 }
 
 // ---- wave-wide reductions: DPP within 16-lane rows, readlane across rows (result wave-uniform) ----
-template <int CTRL>
-__device__ __forceinline__ unsigned long long dpp64(unsigned long long x) {
-    unsigned lo = (unsigned)x, hi = (unsigned)(x >> 32);
-    lo = (unsigned)__builtin_amdgcn_mov_dpp((int)lo, CTRL, 0xf, 0xf, false);
-    hi = (unsigned)__builtin_amdgcn_mov_dpp((int)hi, CTRL, 0xf, 0xf, false);
-    return ((unsigned long long)hi << 32) | lo;
-}
 __device__ __forceinline__ unsigned long long readlane64(unsigned long long x, int l) {
     unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)x, l);
     unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(x >> 32), l);
@@ -734,7 +851,6 @@ __device__ __forceinline__ double bperm_d(double x, int src) {
     const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(unsigned)(b >> 32));
     return as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
 }
-__device__ __forceinline__ unsigned long long umax64(unsigned long long a, unsigned long long b) { return a > b ? a : b; }
 // max over the 64 lanes of a wave (every lane must be active)
 __device__ __forceinline__ unsigned long long wave_max_u64(unsigned long long x) {
     x = umax64(x, dpp64<0xB1>(x));   // quad_perm [1,0,3,2]
@@ -3430,11 +3546,13 @@ __global__ void k_xs_in(const double* __restrict__ b, const double* __restrict__
     }
 }
 __global__ void k_xs_out(const double* __restrict__ xs, const double* __restrict__ scale, const int32_t* __restrict__ xpos,
-                         const uint32_t* __restrict__ abort_flag, double* __restrict__ x, int64_t n, const int32_t* __restrict__ list) {
+                         const uint32_t* __restrict__ abort_flag, double* __restrict__ x, int64_t n, const int32_t* __restrict__ list,
+                         int sub) {
     if (*abort_flag) return;  // aborted dataflow solve: x (possibly aliasing the rhs) is left untouched
     for (int64_t t = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; t < n; t += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = list ? list[t] : t;
-        x[i] = scale[i] * xs[xpos[i]];
+        const double d = __dmul_rn(scale[i], xs[xpos[i]]);  // no contraction into the subtraction
+        x[i] = sub ? x[i] - d : d;
     }
 }
 __global__ void k_xpos_top(const int32_t* __restrict__ top_orig, int64_t n_top, int64_t top_base, int32_t* __restrict__ xpos) {
@@ -4317,6 +4435,16 @@ hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
     return hipGetLastError();
 }
 
+hipError_t launch_resid(const ResidArgs& A, hipStream_t s) {
+    if (A.n == 0) return hipSuccess;
+    if (A.nf > 0)
+        hipLaunchKernelGGL(k_resid_front, dim3((unsigned)A.nf), dim3(64), 16 * (size_t)std::max(A.max_m, 1), s, A);
+    const int64_t threads = A.n_chunks * 64 + A.n * 4;
+    hipLaunchKernelGGL(k_resid_rows, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, s, A);
+    if (A.n_long > 0) hipLaunchKernelGGL(k_resid_long_fin, dim3((unsigned)((A.n_long + 255) / 256)), dim3(256), 0, s, A);
+    return hipGetLastError();
+}
+
 hipError_t launch_rowsum_norm_orig(ScanArgs A, double* rowsum, hipStream_t s) {
     if (A.n == 0) return hipSuccess;
     A.out = rowsum;
@@ -4629,9 +4757,9 @@ hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpo
 }
 
 hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, const uint32_t* abort_flag, double* x,
-                         int64_t n, hipStream_t s, const int32_t* list) {
+                         int64_t n, hipStream_t s, const int32_t* list, bool sub) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, abort_flag, x, n, list);
+    hipLaunchKernelGGL(k_xs_out, dim3(grid_for(n, 256)), dim3(256), 0, s, xs, scale, xpos, abort_flag, x, n, list, sub ? 1 : 0);
     return hipGetLastError();
 }
 

@@ -198,6 +198,8 @@ struct SweepArgs {
     const int32_t* big_list;    // fronts of more than kSweepBigSlots slots (swept by 2-D grids)
     int32_t n_big = 0, big_slices = 1;
     int rmax_zero = 0;  // rmax_all is known to be all zero (k_sweep_final leaves it so): no clearing memset
+    unsigned long long* counters = nullptr;  // reset by the first sweep's block 0 (k_reset_counters' values:
+                                             // one launch less at the head of the factorization)
 };
 hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s);
 hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
@@ -206,6 +208,40 @@ hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const
 hipError_t launch_rowsum_norm_orig(ScanArgs A, double* rowsum, hipStream_t s);
 constexpr int kMaxSweepFront = 4096;  // largest front order of the front sweeps (LDS 16 B per row)
 constexpr int64_t kSweepBigSlots = 16384;  // fronts with more slots are swept by slices (k_sweep_front<., true>)
+
+// Residual r = A x - b of a refinement step (uno_kkt_solve after a factorization with relaxed pivots), over
+// the fronts' packed slots instead of the row-wise COO symv (whose row halves gather every slot a second
+// time, scattered): one wave per front accumulates its slots' products into the front's rows in LDS (one
+// wave: a fixed order), writes one partial per front row, then each row sums its partials in front order
+// (rz_ptr / rz_pos: the front rows that hold a slot of the row): 4 lanes per row up to kResidShort partials,
+// longer rows (separator and dense rows) by chunks of kResidChunk partials, one wave each, whose sums are
+// added in chunk order.  Deterministic.
+struct ResidArgs {
+    int64_t nf, n;
+    const int32_t* fm;
+    const int64_t* rows_off;
+    const int32_t* rows;       // the fronts' rows by original id
+    const int64_t* ent_off;    // nf+1 slot ranges
+    const uint32_t* ent_lpos;  // (lr << 16) | flip << 15 | lc
+    const double* uval;        // packed values (unscaled)
+    const double* x;           // by original id
+    const double* b;           // by original id
+    double* part;              // one partial per front row
+    const int32_t* rz_ptr;     // n+1, by original id
+    const int32_t* rz_pos;     // front-row positions of each row's partials, ascending front
+    int32_t short_len = 0;     // rows with more partials are chunked (kResidShort; smaller in tests)
+    const int32_t* long_rows = nullptr;  // original ids of the chunked rows
+    int32_t n_long = 0;
+    const int32_t* chunk_off = nullptr;  // n_long+1: each chunked row's chunks
+    int64_t n_chunks = 0;
+    const int32_t* chunk_row = nullptr;  // per chunk: index among the chunked rows
+    double* chunk_part = nullptr;        // per chunk: sum of its partials
+    double* r;                 // out, by original id
+    int max_m;
+};
+constexpr int kResidShort = 32;   // 4 lanes x 8 partials
+constexpr int kResidChunk = 256;  // 64 lanes x 4 partials
+hipError_t launch_resid(const ResidArgs& A, hipStream_t s);
 
 // partial scans of the top (separator) rows on one rank: chunk c covers pslot[chunk_begin[c] ..
 // chunk_begin[c+1]) of top row chunk_row[c]; ppartner = original id of the slot's other index
@@ -291,8 +327,9 @@ hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32
 // xs[xpos[i]] = scale_i b_i  /  x_i = scale_i xs[xpos[i]]; rows i = list[0 .. n) (list == nullptr: 0 .. n-1)
 hipError_t launch_xs_in(const double* b, const double* scale, const int32_t* xpos, double* xs, int64_t n, hipStream_t s,
                         const int32_t* list = nullptr);
+// sub: x_i -= scale_i xs[xpos[i]] (a refinement correction, rounded as the product stored and subtracted)
 hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* xpos, const uint32_t* abort_flag, double* x,
-                         int64_t n, hipStream_t s, const int32_t* list = nullptr);
+                         int64_t n, hipStream_t s, const int32_t* list = nullptr, bool sub = false);
 // distributed dataflow solve: subtree roots' update vectors (cvx slots) -> cvec (level-schedule layout,
 // sent to rank 0); done[f] = epoch for the top fronts (the subtree roots' parents) before the backward
 hipError_t launch_cvx_to_cvec(const DfArgs& D, const SolveArgs& A, const int32_t* roots, int count, double* cvec, hipStream_t s);
