@@ -108,6 +108,35 @@ def test_device_rhs_and_direction_bitwise():
 
 
 @pytest.mark.gpu
+def test_device_rhs_long_variables_bitwise():
+    """Variables in more than kRhsLong (1024) constraints -- the arrowband's linking variables are in all of
+    them -- take the one-wave ordered sum (k_rhs_long): bit-identical to the reference's accumulation,
+    zero multipliers skipped, list lengths that are and are not multiples of 64."""
+    import torch
+    import uno_amd
+    rng = np.random.default_rng(8)
+    n, m = 3000, 5000
+    grad, cons, y, jc, jv, jval = random_ipm_point(rng, n, m, nnz_per_con=4)
+    dense = np.array([7, 1500, 2999])                # in every constraint
+    half = np.array([11])                            # in the first 1088 = 17 x 64 constraints
+    jc = np.concatenate([jc, np.repeat(np.arange(m), len(dense)), np.arange(1088)])
+    jv = np.concatenate([jv, np.tile(dense, m), np.repeat(half, 1088)])
+    perm = rng.permutation(len(jc))
+    jc, jv = jc[perm], jv[perm]
+    jval = rng.uniform(-2, 2, size=len(jc))
+    g = uno_amd.HipKKT(0)
+    g.rhs_setup(n, m, jc, jv)
+    d = lambda a: torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).cuda()
+    G, C, Y, JV = d(grad), d(cons), d(y), d(jval)
+    rhs = torch.empty(n + m, dtype=torch.float64, device="cuda")
+    torch.cuda.synchronize()
+    g.assemble_rhs(G.data_ptr(), C.data_ptr(), Y.data_ptr(), JV.data_ptr(), rhs.data_ptr())
+    torch.cuda.synchronize()
+    ref = ipm_oracle.assemble_augmented_rhs(grad, cons, y, jc, jv, jval)
+    np.testing.assert_array_equal(rhs.cpu().numpy(), ref)
+
+
+@pytest.mark.gpu
 def test_device_symv_and_quadratic_product():
     import torch
     import uno_amd

@@ -36,9 +36,10 @@ __device__ __forceinline__ unsigned long long bits(double d) { return (unsigned 
 // of constraints with y_j == 0 are skipped as in the reference (Subproblem.cpp:89).
 __global__ void k_rhs(const double* __restrict__ grad, const double* __restrict__ cons, const double* __restrict__ y,
                       const double* __restrict__ jval, const int64_t* __restrict__ vptr, const int32_t* __restrict__ vent,
-                      const int32_t* __restrict__ jcon, int64_t n, int64_t m, double* __restrict__ rhs) {
+                      const int32_t* __restrict__ jcon, int64_t n, int64_t m, double* __restrict__ rhs, int64_t long_len) {
     for (int64_t i = (int64_t)blockIdx.x * kT + threadIdx.x; i < n + m; i += (int64_t)gridDim.x * kT) {
         if (i < n) {
+            if (vptr[i + 1] - vptr[i] > long_len) continue;  // k_rhs_long
             double r = -grad[i];
             for (int64_t q = vptr[i]; q < vptr[i + 1]; ++q) {
                 const int32_t e = vent[q];
@@ -50,6 +51,56 @@ __global__ void k_rhs(const double* __restrict__ grad, const double* __restrict_
             rhs[i] = -cons[i - n];
         }
     }
+}
+
+// Variables in more than long_len constraints (C3: six linking variables in all 250 000): one thread summing
+// such a list one dependent gather after the other took 163 ms.  One wave per such variable now gathers 64
+// entries at a time (the next 512 in flight), stages the products in LDS and lane 0 adds them in list order,
+// so the sum is the reference's, bit for bit (gathers with a branch per entry, 64 or 256 per chunk: 5.7 / 6.2 ms
+// for 250 000 entries, every gather a round trip of its own; a readlane per term: 15 ms).
+__global__ __launch_bounds__(64) void k_rhs_long(const double* __restrict__ grad, const double* __restrict__ y,
+                                                 const double* __restrict__ jval, const int64_t* __restrict__ vptr,
+                                                 const int32_t* __restrict__ vent, const int32_t* __restrict__ jcon,
+                                                 const int32_t* __restrict__ long_vars, double* __restrict__ rhs) {
+    constexpr int U = 8;  // entries per lane and chunk: 512 per chunk
+    const int lane = threadIdx.x;
+    const int32_t i = long_vars[blockIdx.x];
+    const int64_t q0 = vptr[i], q1 = vptr[i + 1];
+    // y_c * d_e of the chunk's entries, branch-free (indices clamped into the list) so the U gathers of each
+    // dependent step are in flight together; -0.0 where skipped (y_c = 0, or past the list): -0.0 is the exact
+    // identity of the addition (x + -0.0 = x for every x, the sign of a zero sum included), so lane 0 adds
+    // every slot
+    auto chunk = [&](int64_t q, double (&t)[U]) {
+        int32_t e[U], c[U];
+        double yv[U], dv[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) e[u] = vent[min(q + 64 * u + lane, q1 - 1)];
+#pragma unroll
+        for (int u = 0; u < U; ++u) c[u] = jcon[e[u]];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            yv[u] = y[c[u]];
+            dv[u] = jval[e[u]];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) t[u] = (q + 64 * u + lane < q1 && yv[u] != 0.0) ? yv[u] * dv[u] : -0.0;
+    };
+    __shared__ double buf[64 * U];
+    double r = -grad[i];
+    double t[U];
+    chunk(q0, t);
+    for (int64_t q = q0; q < q1; q += 64 * U) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) buf[64 * u + lane] = t[u];
+        __syncthreads();
+        if (q + 64 * U < q1) chunk(q + 64 * U, t);  // the next chunk's gathers under this chunk's sum
+        if (lane == 0) {
+#pragma unroll 64
+            for (int l = 0; l < 64 * U; ++l) r += buf[l];  // list order
+        }
+        __syncthreads();
+    }
+    if (lane == 0) rhs[i] = r;
 }
 
 // direction + fraction-to-boundary step lengths; alpha[0] / alpha[1] hold the bit patterns of the
@@ -290,9 +341,13 @@ hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double*
 }
 
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
-                      const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s) {
+                      const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s,
+                      const int32_t* long_vars, int32_t n_long, int64_t long_len) {
     if (n + m == 0) return hipSuccess;
-    hipLaunchKernelGGL(k_rhs, dim3(grid_of(n + m)), dim3(kT), 0, s, grad, cons, y, jval, vptr, vent, jcon, n, m, rhs);
+    if (n_long == 0) long_len = INT64_MAX;
+    hipLaunchKernelGGL(k_rhs, dim3(grid_of(n + m)), dim3(kT), 0, s, grad, cons, y, jval, vptr, vent, jcon, n, m, rhs, long_len);
+    if (n_long > 0)
+        hipLaunchKernelGGL(k_rhs_long, dim3((unsigned)n_long), dim3(64), 0, s, grad, y, jval, vptr, vent, jcon, long_vars, rhs);
     return hipGetLastError();
 }
 

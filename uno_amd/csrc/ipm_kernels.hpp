@@ -64,8 +64,11 @@ struct AugArgs {
 };
 hipError_t launch_assemble_augmented(const AugArgs& A, hipStream_t s);
 
+// variables with more than long_len entries (long_vars, n_long of them) are summed by k_rhs_long (same order)
 hipError_t launch_rhs(const double* grad, const double* cons, const double* y, const double* jval, const int64_t* vptr,
-                      const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s);
+                      const int32_t* vent, const int32_t* jcon, int64_t n, int64_t m, double* rhs, hipStream_t s,
+                      const int32_t* long_vars, int32_t n_long, int64_t long_len);
+constexpr int64_t kRhsLong = 1024;
 hipError_t launch_direction(const DirArgs& A, hipStream_t s);
 hipError_t launch_barrier(const int32_t* var, const int8_t* which, const double* lb, const double* ub, const double* x,
                           const double* zl, const double* zu, int64_t count, double* values, hipStream_t s);

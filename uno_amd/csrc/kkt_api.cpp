@@ -256,6 +256,8 @@ struct uno_kkt {
     int64_t bar_n = -1;
     int64_t aug_reg = -1, aug_nh = 0, aug_nj = 0;  // uno_kkt_augmented_setup
     DBuf<int32_t> jv_ent, j_con;
+    DBuf<int32_t> rhs_long;               // variables in more than kRhsLong constraints
+    int32_t rhs_n_long = 0;
     DBuf<unsigned long long> alpha;
     DBuf<double> symv_tmp, symv_part, dot_d;
     DBuf<double> xtmp, rtmp;              // host-pointer solves / refinement residuals
@@ -2475,6 +2477,11 @@ int uno_kkt_rhs_setup(uno_kkt_t h, int64_t n_vars, int64_t n_cons, int64_t nnz_j
     HIPCHK(h, h->jv_ptr.upload(ptr, s));
     HIPCHK(h, h->jv_ent.upload(ent, s));
     HIPCHK(h, h->j_con.upload(con, s));
+    std::vector<int32_t> lv;  // variables in more than kRhsLong constraints (k_rhs_long)
+    for (int64_t i = 0; i < n_vars; ++i)
+        if (ptr[i + 1] - ptr[i] > kRhsLong) lv.push_back((int32_t)i);
+    h->rhs_n_long = (int32_t)lv.size();
+    if (!lv.empty()) HIPCHK(h, h->rhs_long.upload(lv, s));
     HIPCHK(h, hipStreamSynchronize(s));
     h->rhs_n = n_vars;
     h->rhs_m = n_cons;
@@ -2553,7 +2560,7 @@ int uno_kkt_assemble_rhs(uno_kkt_t h, const double* grad, const double* cons, co
     if (h->rhs_n < 0) return set_err(h, UNO_KKT_ERR_STATE, "assemble_rhs before rhs_setup");
     HIPCHK(h, hipSetDevice(h->device));
     HIPCHK(h, launch_rhs(grad, cons, y, jac_values, h->jv_ptr.p, h->jv_ent.p, h->j_con.p, h->rhs_n, h->rhs_m, rhs,
-                         h->stream));
+                         h->stream, h->rhs_long.p, h->rhs_n_long, kRhsLong));
     return UNO_KKT_OK;
 }
 
