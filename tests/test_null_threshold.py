@@ -103,3 +103,70 @@ def test_relaxed_vs_delayed_pivots(exps):
         assert rel_residual(n, r, c, v, x, b) < 1e-10, relaxed
         np.testing.assert_allclose(x, xo, rtol=1e-8, atol=1e-10 * np.abs(xo).max())
         g.close()
+
+
+def relaxed_mode_case(seed):
+    """delay_case's hub-and-spokes fronts (every fully-summed pivot below u) with random sizes, random
+    exponents, random signs and a random sparse symmetric coupling among the spokes (so 2x2 candidates exist
+    and the fronts' blocks are no longer diagonal); the dense matrix for numpy's eigenvalues."""
+    from kkt_cases import delay_case
+    rng = np.random.default_rng(1000 + seed)
+    N = int(rng.integers(120, 400))
+    exps = list(rng.integers(-9, -2, size=int(rng.integers(1, 4))))
+    n, r, c, v, _ = delay_case(N, exps, seed=seed)
+    k = N // 2
+    pr = rng.integers(0, N, k)
+    pc = np.minimum(N - 1, pr + rng.integers(1, 6, k))  # couplings between nearby spokes
+    pv = rng.choice([-1.0, 1.0], k) * 10.0 ** rng.uniform(-3, -1, k)
+    r, c, v = np.concatenate([r, pc]), np.concatenate([c, pr]), np.concatenate([v, pv])
+    D = np.zeros((n, n))
+    np.add.at(D, (r, c), v)
+    D = D + D.T - np.diag(np.diag(D))
+    return n, r.astype(np.int64), c.astype(np.int64), v, D
+
+
+@pytest.mark.gpu
+def test_relaxed_mode_random_cases():
+    """VERDICT r4 (parity 1d): the shipped mode (delay_relaxed = 0, threshold relaxation + one refinement step)
+    beyond the three constructed cases: 12 random hub-and-spokes systems whose fronts only have pivots below u,
+    with random couplings.  Per case the inertia equals numpy's eigenvalue count and the oracle's (MUMPS
+    delays), the refined solution meets the residual and componentwise backward-error bars, and relaxed
+    pivots were actually taken."""
+    import uno_amd
+    from test_gpu_parity import rel_residual, componentwise_backward_error, OMEGA_TOL
+    uno_amd.load_library()
+    relaxed_total = 0
+    for seed in range(12):
+        n, r, c, v, D = relaxed_mode_case(seed)
+        ev = np.linalg.eigvalsh(D)
+        truth = (int((ev > 0).sum()), int((ev < 0).sum()), 0)
+        assert np.abs(ev).min() > 1e-13 * np.abs(ev).max(), seed  # eigenvalues far above the rounding level
+        o = OracleKKT()
+        o.analyze(n, r, c)
+        o.factorize(v)
+        assert o.inertia() == truth, seed
+        g = uno_amd.HipKKT(0, delay_relaxed=0)
+        g.analyze(n, r, c)
+        g.factorize(v)
+        assert g.inertia() == truth, (seed, g.inertia(), truth)
+        st = g.stats()
+        assert st["fronts_merged"] == 0
+        relaxed_total += st["pivots_relaxed"]
+        b = np.cos(np.arange(n, dtype=np.float64) * 0.37 + seed)
+        x = g.solve(b)
+        assert rel_residual(n, r, c, v, x, b) < 1e-10, seed
+        assert componentwise_backward_error(n, r, c, v, x, b) < OMEGA_TOL, seed
+        g.close()
+    assert relaxed_total > 0
+
+
+def test_oracle_relaxed_mode_cases():
+    """CPU: the oracle's inertia (MUMPS delays) on the random hub-and-spokes cases equals numpy's eigenvalue
+    count -- the truth test_relaxed_mode_random_cases holds the GPU's relaxed mode to."""
+    for seed in range(12):
+        n, r, c, v, D = relaxed_mode_case(seed)
+        ev = np.linalg.eigvalsh(D)
+        o = OracleKKT()
+        o.analyze(n, r, c)
+        o.factorize(v)
+        assert o.inertia() == (int((ev > 0).sum()), int((ev < 0).sum()), 0), seed
