@@ -141,6 +141,17 @@ def run_ipm(args):
     yv = torch.empty(m, dtype=torch.float64, device=dev)
     dx, dzl, dzu = torch.empty_like(xs), torch.empty_like(xs), torch.empty_like(xs)
     dy = torch.empty_like(yv)
+    # the synthetic model's Hessian (symmetric) and Jacobian as device CSR matrices, built once (the values are
+    # fixed): its gradient and constraints are two sparse matrix-vector products per iteration
+    try:
+        hrow = torch.cat([hr, hc_off])
+        hcol = torch.cat([hc, hr_off])
+        hval = torch.cat([hess_d, hess_d[hoff]])
+        H_csr = torch.sparse_coo_tensor(torch.stack([hrow, hcol]), hval, (nv, nv)).coalesce().to_sparse_csr()
+        J_csr = torch.sparse_coo_tensor(torch.stack([jc_d, jr_d]), jac_d, (m, nv)).coalesce().to_sparse_csr()
+        _ = H_csr @ gvec
+    except Exception:  # no sparse kernels: the scatter form
+        H_csr = J_csr = None
     gen = torch.Generator(device=dev)
     gen.manual_seed(11)
     gvec.uniform_(-1.0, 1.0, generator=gen)
@@ -158,11 +169,15 @@ def run_ipm(args):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         # model evaluation on the device (ArrowbandModel: gradient H x + g, constraints A x - b with b = 0 here)
-        grad.copy_(gvec)
-        grad.index_add_(0, hr, hess_d * xs[hc])
-        grad.index_add_(0, hc_off, hess_d[hoff] * xs[hr_off])
-        cons.zero_()
-        cons.index_add_(0, jc_d, jac_d * xs[jr_d])
+        if H_csr is not None:
+            torch.add(gvec, H_csr @ xs, out=grad)
+            cons.copy_(J_csr @ xs)
+        else:
+            grad.copy_(gvec)
+            grad.index_add_(0, hr, hess_d * xs[hc])
+            grad.index_add_(0, hc_off, hess_d[hoff] * xs[hr_off])
+            cons.zero_()
+            cons.index_add_(0, jc_d, jac_d * xs[jr_d])
         torch.cuda.current_stream().synchronize()
         t_model.append(time.perf_counter() - t0)
         with torch.cuda.stream(stream):
