@@ -53,6 +53,17 @@ if os.environ.get("MODE") == "5":  # tile kernels: shader cycles per front of ea
               f"pivots {c[:,1].mean():7.0f} stage+mfma {c[:,2].mean():7.0f} lds-steps {c[:,3].mean():7.0f} | "
               f"assemble {asm[s].mean():6.2f} loop {loop[s].mean():6.2f} write {wout[s].mean():5.2f} us")
     sys.exit(0)
+if os.environ.get("MODE") == "8":  # LDS-path pivot steps by phase (a UKKT_STEP_STAMPS build)
+    n_l = st[:, 7] >> 40
+    for lev in range(fl.max() + 1):
+        s = fl == lev
+        nl = n_l[s].astype(np.float64)
+        tot = nl.sum()
+        per = lambda col: (st[s, col].sum() / max(tot, 1))
+        rel = ((st[s, 7] & 0xffffffffff).sum() / max(tot, 1))
+        print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | LDS steps/front {nl.mean():5.2f} | cycles per LDS step: "
+              f"spill {per(4):6.0f} search {per(5):6.0f} swap+update {per(6):6.0f} reload {rel:6.0f} | loop {loop[s].mean():6.2f} us")
+    sys.exit(0)
 if os.environ.get("MODE") == "3":
     w4, w5 = st[:, 4], st[:, 5]
     parts = np.stack([w4 & 0xffffffff, w4 >> 32, w5 & 0xffffffff, w5 >> 32, st[:, 6]], 1).astype(np.float64)

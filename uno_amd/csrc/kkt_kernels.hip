@@ -1362,9 +1362,12 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // pivot step); the phase stamps (assembly / loop / write-out) need no flag here
 #ifdef UKKT_STEP_STAMPS
     const bool stamping = A.stamps != nullptr && A.stamp_mode != 7;
+    const bool st8 = A.stamps != nullptr && A.stamp_mode == 8;  // LDS-path steps by phase (stamps.py MODE=8)
 #else
     constexpr bool stamping = false;
+    constexpr bool st8 = false;
 #endif
+    unsigned long long ls_spill = 0, ls_search = 0, ls_upd = 0, ls_reload = 0, t8 = 0;
     int k = 0;
     constexpr bool REG = MR > 0;
     constexpr int RM = MR > 0 ? MR : 1;
@@ -1409,32 +1412,35 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     const bool owner = tx == kk;
                     const double akk = readlane_d(R[bk][bk], kk * G + kk);
                     const double aak = fabs(akk);
-                    const double dinv = 1.0 / akk;  // issued before the test: overlaps it
+                    const double dinv = 1.0 / akk;
                     // the owners (tx == kk) publish column k (padding rows are 0: stored as is) and test
                     // each candidate: "some u |a_ik| > |a_kk|" is exactly u * max_i |a_ik| > |a_kk| (the
                     // rounding of u * x is monotonic in x); rows <= k of the diagonal block are excluded
                     // (a max-reduction first would be one product and one compare, but maxnum of loaded values
                     // costs a canonicalize per element in IEEE mode: 17 dependent DP ops instead of 16 independent)
-                    bool bad = false;
+                    // the test's compares are counted in a VGPR (independent v_cndmask / v_add, not a v_cmp -> s_or chain
+                    // through the scalar unit)
+                    int nbad = 0;
                     if (owner) {
 #pragma unroll
                         for (int a = bk; a < RM; ++a) colw[ty + G * a] = R[a][bk];
 #pragma unroll
-                        for (int a = bk; a < RM; ++a) bad |= (a > bk || ty > kk) && A.u * fabs(R[a][bk]) > aak;
+                        for (int a = bk; a < RM; ++a) nbad += ((a > bk || ty > kk) && A.u * fabs(R[a][bk]) > aak) ? 1 : 0;
                     }
-                    need = (__ballot(bad) != 0) || !(aak > thres);
+                    // the update's operands read now, whatever the test says (the column was just published: in-wave
+                    // LDS order), so their latency runs under the division and the ballot instead of after them
+                    double lv[RM], cw[RM];
+#pragma unroll
+                    for (int a = bk; a < RM; ++a) {
+                        lv[a] = colw[ty + G * a];
+                        cw[a] = colw[tx + G * a];
+                    }
+                    need = (__ballot(nbad != 0) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange (k < 64: its |a_kk| enters minpiv after the loop)
-                        double lv[RM], cv[RM];
+                        double cv[RM];
 #pragma unroll
-                        for (int a = bk; a < RM; ++a) {
-                            lv[a] = colw[ty + G * a];
-#ifdef UKKT_DIAG_HALF_LDS
-                            cv[a] = lv[a] * dinv;  // DIAGNOSTIC build only (wrong results): half the LDS operand reads
-#else
-                            cv[a] = colw[tx + G * a] * dinv;
-#endif
-                        }
+                        for (int a = bk; a < RM; ++a) cv[a] = cw[a] * dinv;
                         if (tx <= kk) cv[bk] = 0.0;  // columns <= k keep their values
 #pragma unroll
                         for (int a = bk; a < RM; ++a)
@@ -1455,8 +1461,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             }
             if (!need) break;
             spilled = true;
+            if (st8) t8 = __builtin_amdgcn_s_memtime();
             reg_store<G, RM>(st, m, R);
             __syncthreads();
+            if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_spill += t - t8; t8 = t; }
         } else if constexpr (REG) {
             const int ty = tid / G, tx = tid % G;
             bool need = false;
@@ -1543,6 +1551,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         }
         __syncthreads();
         if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
+        if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_search += t - t8; t8 = t; }
         PivotDecision d = sh->dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
@@ -1599,7 +1608,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             __syncthreads();
             k += 2;
         }
+        if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_upd += t - t8; t8 = t; }
         if constexpr (REG) reg_load<G, RM>(st, m, R);
+        if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_reload += t - t8; t8 = t; }
     }
     if constexpr (REG && W == 1) {
         // pivot kinds and inertia counts of the register path's 1x1 steps (recorded as bit masks in the loop)
@@ -1655,7 +1666,12 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
-        if (!sub && A.stamp_mode != 4) {
+        if (st8) {
+            A.stamps[8 * f + 4] = ls_spill;
+            A.stamps[8 * f + 5] = ls_search;
+            A.stamps[8 * f + 6] = ls_upd;
+            A.stamps[8 * f + 7] = ((unsigned long long)nlds << 40) | (ls_reload & 0xffffffffffull);
+        } else if (!sub && A.stamp_mode != 4) {
             A.stamps[8 * f + 4] = cyc_search;
             A.stamps[8 * f + 5] = cyc_update;
             A.stamps[8 * f + 6] = cyc_rest;
