@@ -152,6 +152,9 @@ struct uno_kkt {
     DBuf<int32_t> dup_ptr, dup_pos, ent_r, ent_c, fm, fp, rows, frow, fpos, child_off, child, relmap, fstat;
     DBuf<uint32_t> ent_lpos;
     DBuf<int64_t> rows_off, ent_off, relmap_off, L_off, cb_off, gscratch_off, ch_relmap_off, ch_cb_off;
+    DBuf<uint16_t> cbpos;                 // FactorArgs::cbpos
+    bool use_cbpos = false;
+    int cbpos_opt = 1;                    // option "cbpos"
     DBuf<int32_t> ch_cm;
     DBuf<int8_t> piv;
     DBuf<BigFrontState> big;              // large-front factorization state (fronts with m > kMaxLdsFront)
@@ -1214,6 +1217,30 @@ int upload_structure(uno_kkt_t h) {
     HIPCHK(h, h->relmap.upload(S.relmap, s));
     HIPCHK(h, h->L_off.upload(S.f_L_off, s));
     HIPCHK(h, h->cb_off.upload(S.f_cb_off, s));
+    {  // cbpos: each contribution-block entry's packed position i (i + 1) / 2 + j in its parent's LDS front
+        h->use_cbpos = false;
+        if (h->cbpos_opt && S.cb_size > 0 && S.cb_size < INT32_MAX) {
+            std::vector<uint16_t> cp((size_t)S.cb_size, 0);
+            bool ok = true;
+            for (int64_t c = 0; c < S.nf && ok; ++c) {
+                const int32_t par = S.f_parent[c];
+                if (par < 0 || S.f_m[par] > kMaxLdsFront) continue;  // roots; large parents use k_big_child
+                const int cm = S.f_m[c] - S.f_p[c];
+                const int32_t* rm = S.relmap.data() + S.f_relmap_off[c];
+                int64_t t = S.f_cb_off[c];
+                for (int r = 0; r < cm; ++r) {
+                    const int64_t i = rm[r], base = i * (i + 1) / 2;
+                    if (base + i >= 65536) { ok = false; break; }
+                    for (int q = 0; q <= r; ++q) cp[t++] = (uint16_t)(base + rm[q]);
+                }
+            }
+            if (ok) {
+                HIPCHK(h, h->cbpos.upload(cp, s));
+                HIPCHK(h, hipStreamSynchronize(s));
+                h->use_cbpos = true;
+            }
+        }
+    }
     HIPCHK(h, h->gscratch_off.upload(goff, s));
     HIPCHK(h, h->fstat.alloc(S.nf));
     HIPCHK(h, h->fcnt.alloc(S.nf));
@@ -1461,6 +1488,7 @@ int enqueue_factorization(uno_kkt_t h) {
     A.child_off = h->child_off.p; A.child = h->child.p; A.relmap_off = h->relmap_off.p; A.relmap = h->relmap.p;
     A.ch_cm = h->ch_cm.p; A.ch_relmap_off = h->ch_relmap_off.p; A.ch_cb_off = h->ch_cb_off.p;
     A.L_off = h->L_off.p; A.cb_off = h->cb_off.p; A.gscratch_off = h->gscratch_off.p; A.anorm_bits = h->anorm_p;
+    A.cbpos = h->use_cbpos ? h->cbpos.p : nullptr;
     A.L = h->L.p; A.cb = h->cb.p; A.gscratch = h->gscratch.p; A.frow = h->frow.p; A.fpos = h->fpos.p; A.piv = h->piv.p;
     A.counters = h->counters.p; A.fstat = h->fstat.p; A.fslow = h->fslow.p; A.fcnt = h->fcnt.p; A.u = h->u; A.null_fac = h->null_fac;
     A.fmin = h->fmin.p;
@@ -1678,6 +1706,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "refine_tol") h->refine_tol = std::max(0.0, value);
     else if (n == "sweep_reset") h->sweep_reset = value != 0.0;
+    else if (n == "cbpos") h->cbpos_opt = value != 0.0;  // takes effect at the next analysis
     else if (n == "resid_fronts") { h->resid_fronts = value != 0.0; h->rz_state = 0; }
     else if (n == "resid_long") { h->resid_long = std::max<int64_t>(1, (int64_t)value); h->rz_state = 0; }
     else if (n == "pin_host_values") h->pin_host = value != 0.0;

@@ -1952,7 +1952,16 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
         double v[CB];
         int pos[CB];
     };
-    auto load_batch = [&](const double* cb, const int32_t* rm, int ctot, int t0, Batch& b) {
+    auto load_batch = [&](const double* cb, const int32_t* rm, const uint16_t* cp, int ctot, int t0, Batch& b) {
+        if (cp) {  // the entries' positions in this front, precomputed (FactorArgs::cbpos): no relmap gathers
+#pragma unroll
+            for (int u = 0; u < CB; ++u) {
+                const int t = t0 + u * NT;
+                b.v[u] = t < ctot ? (DF ? ld_sc1(cb + t) : cb[t]) : 0.0;
+                b.pos[u] = t < ctot ? (int)cp[t] : -1;
+            }
+            return;
+        }
         int32_t gi[CB], gj[CB];
 #pragma unroll
         for (int u = 0; u < CB; ++u) {
@@ -1988,21 +1997,23 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
             const double* cba = A.cb + (int64_t)readlane64(my_cbo, q);
             const int32_t* rmb = A.relmap + (two ? (int64_t)readlane64(my_rmo, q + 1) : 0);
             const double* cbb = A.cb + (two ? (int64_t)readlane64(my_cbo, q + 1) : 0);
+            const uint16_t* cpa = A.cbpos ? A.cbpos + (int64_t)readlane64(my_cbo, q) : nullptr;
+            const uint16_t* cpb = A.cbpos && two ? A.cbpos + (int64_t)readlane64(my_cbo, q + 1) : nullptr;
             const int ta = cma > 0 ? cma * (cma + 1) / 2 : 0, tb = cmb > 0 ? cmb * (cmb + 1) / 2 : 0;
             Batch ba, bb;
-            load_batch(cba, rma, ta, tid, ba);
-            load_batch(cbb, rmb, tb, tid, bb);
+            load_batch(cba, rma, cpa, ta, tid, ba);
+            load_batch(cbb, rmb, cpb, tb, tid, bb);
             add_batch(ba);
             // rest of a / b (CBs of more than 45 rows at one wave): uniform loops, so the barrier
             // below is reached by every wave
             for (int base = NT * CB; base < ta; base += NT * CB) {
-                load_batch(cba, rma, ta, base + tid, ba);
+                load_batch(cba, rma, cpa, ta, base + tid, ba);
                 add_batch(ba);
             }
             if (NT > 64) __syncthreads();  // children may overlap: one child at a time
             add_batch(bb);
             for (int base = NT * CB; base < tb; base += NT * CB) {
-                load_batch(cbb, rmb, tb, base + tid, bb);
+                load_batch(cbb, rmb, cpb, tb, base + tid, bb);
                 add_batch(bb);
             }
             if (NT > 64) __syncthreads();

@@ -84,6 +84,8 @@ struct FactorArgs {
     uint32_t* df_ticket;        // block start order (cumulative: (epoch - 1) * df_nf at launch)
     uint32_t* df_abort;         // set when a wait exceeded its limit (factorization invalid, host redoes it)
     BigFrontState* big;         // per front: state of the blocked large-front factorization (m > kMaxLdsFront)
+    const uint16_t* cbpos = nullptr;  // per contribution-block entry (layout of cb): its packed position in the
+                                      // parent's LDS front (assemble_front without relmap gathers); nullptr: gathers
     int32_t* xpos = nullptr;        // one GPU, dataflow solve: xpos[row] = xs slot of each pivot (k_xpos pass 0)
     const int64_t* xs_off = nullptr;  // per front: its xs slot (DfArgs::xs_off)
 };
