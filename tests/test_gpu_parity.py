@@ -550,3 +550,21 @@ def test_dataflow_abort_redone_and_rearmed(uno_amd):
     np.testing.assert_array_equal(g.solve(b), x_ref)  # a normal dataflow solve again
     st = g.stats()
     assert st["solve_aborts"] == 2 and st["solve_grid"] > 0
+
+
+@pytest.mark.gpu
+def test_children_assembly_positions_bitwise(uno_amd):
+    """Children assembly through the precomputed packed positions (option cbpos, default on; rebuilt with the
+    structure after delays) adds the same entries in the same order as the relmap-gather form: same inertia,
+    same solution bit for bit, default and relaxed (plugin) mode."""
+    from uno_amd import HipKKT, arrowband, SEEDS
+    N, nv, m, r, c, v, b = arrowband(20000, SEEDS["C2"])
+    for opts in ({}, {"delay_relaxed": 0}):
+        g, ref = HipKKT(0, **opts), HipKKT(0, cbpos=0, **opts)
+        for h in (g, ref):
+            h.analyze(N, r, c)
+            h.factorize(v)
+        assert g.inertia() == ref.inertia()
+        np.testing.assert_array_equal(g.solve(b), ref.solve(b))
+        g.close()
+        ref.close()
