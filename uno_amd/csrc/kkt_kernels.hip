@@ -844,6 +844,20 @@ __device__ __forceinline__ unsigned long long readlane64(unsigned long long x, i
     return ((unsigned long long)hi << 32) | lo;
 }
 __device__ __forceinline__ double readlane_d(double x, int l) { return as_double(readlane64(as_bits(x), l)); }
+// Cross-lane hand-off through LDS inside ONE wave.  The hardware executes a wave's LDS operations in issue order,
+// but the compiler reasons per lane: a plain LDS store by some lanes followed by plain loads of the same words in
+// other lanes is a data race to it, so it may move a load above the store.  Round 5 hit exactly that (ISA diff in
+// DESIGN.md §4 round 6): with the operand reads scheduled ahead of the ballot, LLVM forwarded the owner lanes' own
+// stores into their loads and turned "if (owner) publish; read" into "if (!owner) read; else publish", running the
+// non-owners' branch -- and their LDS reads -- BEFORE the owners' stores: stale operands, wrong inertia on the 5x5
+// known answer.  A wavefront-scope release / wave barrier / acquire orders every LDS access before it against every
+// one after it for all lanes of the wave, and costs no instruction on gfx950 (wavefront-scope fences emit nothing;
+// the "local" address-space tag leaves global loads free to move across it).  Put it between a publish and its read-back, and before a buffer is rewritten.
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
 // x of lane `src` (any lane pattern, one LDS-crossbar round trip, no LDS allocation, no barrier)
 __device__ __forceinline__ double bperm_d(double x, int src) {
     const unsigned long long b = as_bits(x);
@@ -1398,7 +1412,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of
             // the lanes with tx = k % G.  Those lanes test it in place (one compare per row block,
             // one ballot) and publish it to an LDS vector (one store per block) that every lane reads
-            // back as its row / column operands (in-wave LDS ordering: no barrier); the rank-1 update
+            // back as its row / column operands (wave_lds_sync between: no workgroup barrier); the rank-1 update
             // stays in registers.  Rows <= k of column k are never read back (upper-triangle register
             // slots are scratch) and column k itself is left untouched, so L is written from the
             // registers after the loop.
@@ -1421,14 +1435,18 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     // the test's compares are counted in a VGPR (independent v_cndmask / v_add, not a v_cmp -> s_or chain
                     // through the scalar unit)
                     int nbad = 0;
+                    wave_lds_sync();  // the previous step's reads of colw are done before it is rewritten
                     if (owner) {
 #pragma unroll
                         for (int a = bk; a < RM; ++a) colw[ty + G * a] = R[a][bk];
 #pragma unroll
                         for (int a = bk; a < RM; ++a) nbad += ((a > bk || ty > kk) && A.u * fabs(R[a][bk]) > aak) ? 1 : 0;
                     }
-                    // the update's operands read now, whatever the test says (the column was just published: in-wave
-                    // LDS order), so their latency runs under the division and the ballot instead of after them
+                    // publish -> read-back across lanes: explicit (see wave_lds_sync; without it the compiler may
+                    // legally run the non-owners' reads before the owners' stores)
+                    wave_lds_sync();
+                    // the update's operands read now, whatever the test says, so their latency can run under the
+                    // division and the ballot
                     double lv[RM], cw[RM];
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
@@ -3191,6 +3209,7 @@ __device__ __forceinline__ void rg_extend_add(const SolveArgs& A, const DfArgs& 
         }
 #pragma unroll
         for (int u = 0; u < CH; ++u) {  // children in order (rows of one child are distinct)
+            wave_lds_sync();  // the previous child's (or the caller's) LDS writes before these cross-lane reads
             if (rw[u] >= 0) y[fpl[rw[u]]] += v[u];
             if (cms[u] > 64) {  // uniform: the child's rows 64..
                 const int q = (cb - c0) % 64 + u;
@@ -3243,6 +3262,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const unsigned long long twoAM = __ballot(lane < p && q.piv == PIV_2X2_A);
         const int piv_c = q.piv;
         const double dgl = q.dgl, sbl = q.sbl;
+        wave_lds_sync();  // the previous front's reads of y, fpl and Th are done before they are rewritten
         if (m > 64) {  // uniform
 #pragma unroll
             for (int c = 0; c < 4; ++c)
@@ -3257,6 +3277,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
             if ((int32_t)(q.dep - target) < 0) df_wait(D.cnt + f, target, D.abort_flag);
             rg_extend_add(A, D, r.c0, r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
         }
+        wave_lds_sync();  // y, fpl and Th were written by other lanes
         double y0 = y[lane];
         double a1 = m > 64 ? y[lane + 64] : 0.0;
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
@@ -3826,7 +3847,7 @@ __device__ __forceinline__ void each_index(F& f, std::integer_sequence<int, I...
 
 // One wave (lane = row).  Pivot c's d, block-local column maximum, off-diagonal and kind stay in lane c's
 // registers until the loop ends: a global store per step would make every step's barrier wait for its
-// completion.  One wave: its LDS operations complete in issue order, so the column broadcast needs no barrier.
+// completion.  One wave: the column broadcast needs no workgroup barrier, only wave_lds_sync (compiler ordering).
 // The 64 steps are expanded at compile time (each_index): a[] indices stay constants, i.e. registers (the plain
 // unrolled loop with the 2x2 branch passes the full-unroll limit, and the rolled one indexes a[] from scratch).
 // The tests run on upper bounds of the column maxima (wave_max_abs_ub), recorded as such: conservative by 2^-20
@@ -3866,10 +3887,10 @@ __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __
             gmine = lane == c ? g : gmine;
             const double l = lane > c ? a[c] * (1.0 / akk) : 0.0;
             colc[lane] = a[c];  // W(k + lane, c)
-            __asm__ volatile("" ::: "memory");
+            wave_lds_sync();
 #pragma unroll
             for (int j = c + 1; j < kAppNB; ++j) a[j] -= l * colc[j];
-            __asm__ volatile("" ::: "memory");
+            wave_lds_sync();
             return;
         }
         // 2x2 with the next column, no interchange: Duff-Reid's 2x2 test (oracle test_pivot's inequalities) on the
@@ -3894,10 +3915,10 @@ __global__ __launch_bounds__(64) void k_app_diag(FactorArgs A, const int32_t* __
                 const double l1 = lane > c + 1 ? (akk * a[cn] - b * a[c]) * inv : 0.0;
                 colc[lane] = a[c];
                 colc1[lane] = a[cn];
-                __asm__ volatile("" ::: "memory");
+                wave_lds_sync();
 #pragma unroll
                 for (int j = c + 2; j < kAppNB; ++j) a[j] -= l0 * colc[j] + l1 * colc1[j];
-                __asm__ volatile("" ::: "memory");
+                wave_lds_sync();
                 second = true;
                 return;
             }
