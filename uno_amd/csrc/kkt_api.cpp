@@ -574,6 +574,10 @@ int reorder_slow_first(uno_kkt_t h) {
     auto by_slow = [&](int32_t a, int32_t b) { return slow[a] > slow[b]; };
     for (Plan* P : {&h->plan[0], &h->plan[1], &h->dff_plan}) {
         if (P->fac_host.empty()) continue;
+        if (P == &h->dff_plan && h->dff_level == INT32_MAX) continue;  // no dataflow factor: its plan is unused
+        bool valid = true;
+        for (int32_t f : P->fac_host) valid = valid && f >= 0 && f < S.nf;
+        if (!valid) return set_err(h, UNO_KKT_ERR_HIP, "internal: launch list holds front ids of another structure");
         bool any = false;
         for (const Launch& L : P->fac) {
             if (L.global || L.count < 2) continue;  // large fronts keep their host-driven order
@@ -588,6 +592,8 @@ int reorder_slow_first(uno_kkt_t h) {
         if (any) HIPCHK(h, P->fac_fronts.upload(P->fac_host, h->stream));
     }
     if (h->dff_level != INT32_MAX && !h->dff_order_host.empty()) {
+        for (int32_t f : h->dff_order_host)
+            if (f < 0 || f >= S.nf) return set_err(h, UNO_KKT_ERR_HIP, "internal: dataflow order of another structure");
         std::stable_sort(h->dff_order_host.begin(), h->dff_order_host.end(), [&](int32_t a, int32_t b) {
             if (S.f_level[a] != S.f_level[b]) return S.f_level[a] < S.f_level[b];  // children before parents
             return slow[a] > slow[b];
@@ -948,6 +954,11 @@ hipError_t setup_factor_dataflow(uno_kkt_t h) {
     const Symbolic& S = h->S;
     h->dff_level = INT32_MAX;
     h->dff_epoch = 0;
+    // a plan or order of an earlier structure must not survive an early return (reorder_slow_first walks them)
+    h->dff_plan.fac.clear();
+    h->dff_plan.fac_host.clear();
+    h->dff_plan.sol.clear();
+    h->dff_order_host.clear();
     if (!h->dff_enabled || S.nf == 0) return hipSuccess;
     // the fronts of plan[0]: all fronts on one GPU, the rank's own subtrees in a distributed run (the
     // top fronts are factored after the root exchange by the level launches of plan[1])
@@ -2318,6 +2329,10 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         }
         return UNO_KKT_OK;
     };
+    // the statistics of a refined solve whose dataflow walk aborted are rolled back before the redo (its x, residual
+    // and omega were computed from an x the aborted walk never wrote)
+    const int64_t ref0 = h->st.refinements, refskip0 = h->st.refinements_skipped;
+    const double omega0 = h->st.last_backward_error;
     int rc = refined_solve(true);
     if (rc != UNO_KKT_OK) return rc;
     if (refine > 0 && h->df_enabled && h->df_grid > 0) {
@@ -2326,6 +2341,9 @@ int uno_kkt_solve(uno_kkt_t h, const double* rhs, double* x, int on_device) {
         if (dataflow_aborted(h)) {
             if (h->df_abort.p) HIPCHK(h, hipMemsetAsync(h->df_abort.p, 0, sizeof(uint32_t), s));
             if (h->verbose) fprintf(stderr, "[uno_kkt] dataflow solve aborted: the refined solve redone level by level\n");
+            h->st.refinements = ref0;
+            h->st.refinements_skipped = refskip0;
+            h->st.last_backward_error = omega0;
             if ((rc = refined_solve(false)) != UNO_KKT_OK) return rc;
         }
     }
@@ -2573,6 +2591,11 @@ int uno_kkt_assemble_augmented(uno_kkt_t h, double hess_scale, const double* hes
         const int rc = finish_factorization(h);
         if (rc != UNO_KKT_OK && rc != UNO_KKT_ERR_PIVOT) return rc;
     }
+    // the layout is re-checked here: a barrier_setup with another bound count or a re-analysis after
+    // augmented_setup would otherwise let the kernel write past the analysed value array
+    if (h->analyzed && h->aug_reg + h->aug_nh + h->bar_n + h->aug_nj != h->S.nnz)
+        return set_err(h, UNO_KKT_ERR_ARG, "augmented layout (" + std::to_string(h->aug_reg + h->aug_nh + h->bar_n + h->aug_nj) +
+                                           " entries) does not match the analysed nnz " + std::to_string(h->S.nnz));
     AugArgs A;
     A.reg = h->aug_reg; A.nh = h->aug_nh; A.nb = h->bar_n; A.nj = h->aug_nj;
     A.hscale = hess_scale; A.hess = hess; A.jac = jac;

@@ -229,21 +229,27 @@ class HipKKT:
     def inertia(self):
         p, q, z = ctypes.c_int64(), ctypes.c_int64(), ctypes.c_int64()
         self._check(self.lib.uno_kkt_inertia(self.h, ctypes.byref(p), ctypes.byref(q), ctypes.byref(z)))
-        if getattr(self, "_v_in_flight", None):
-            # the factorization is complete: its staged / updated sources were consumed.  A buffer the library
-            # page-locked stays referenced by _v_keep / the list's last entry until another one replaces it
-            self._v_in_flight = self._v_in_flight[-1:]
+        self._factor_consumed()
         return (p.value, q.value, z.value)
+
+    def _factor_consumed(self):
+        """The factorization is complete (inertia / solve waited for it): its staged / updated sources were
+        consumed.  A buffer the library page-locked stays referenced by _v_keep / the list's last entry until
+        another one replaces it."""
+        if getattr(self, "_v_in_flight", None):
+            self._v_in_flight = self._v_in_flight[-1:]
 
     def solve(self, rhs):
         b, _ = _f64(rhs)
         x = np.zeros(self.n, dtype=np.float64)
         self._check(self.lib.uno_kkt_solve(self.h, b.ctypes.data_as(ctypes.c_void_p),
                                            x.ctypes.data_as(ctypes.c_void_p), 0))
+        self._factor_consumed()
         return x
 
     def solve_device(self, rhs_ptr, x_ptr):
         self._check(self.lib.uno_kkt_solve(self.h, ctypes.c_void_p(int(rhs_ptr)), ctypes.c_void_p(int(x_ptr)), 1))
+        self._factor_consumed()  # uno_kkt_solve finishes the queued factorization before it enqueues the solve
 
     def debug_comm_trace(self, clear=False):
         """Transport calls recorded since the last clear (option comm_trace=1): list of (op, peer, bytes, redop),
