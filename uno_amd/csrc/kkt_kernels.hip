@@ -1426,34 +1426,38 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     const bool owner = tx == kk;
                     const double akk = readlane_d(R[bk][bk], kk * G + kk);
                     const double aak = fabs(akk);
-                    const double dinv = 1.0 / akk;
-                    // the owners (tx == kk) publish column k (padding rows are 0: stored as is) and test
-                    // each candidate: "some u |a_ik| > |a_kk|" is exactly u * max_i |a_ik| > |a_kk| (the
-                    // rounding of u * x is monotonic in x); rows <= k of the diagonal block are excluded
-                    // (a max-reduction first would be one product and one compare, but maxnum of loaded values
-                    // costs a canonicalize per element in IEEE mode: 17 dependent DP ops instead of 16 independent)
-                    // the test's compares are counted in a VGPR (independent v_cndmask / v_add, not a v_cmp -> s_or chain
-                    // through the scalar unit)
-                    int nbad = 0;
+                    // the owners (tx == kk) publish column k (padding rows are 0: stored as is); every lane then
+                    // reads back its row / column operands and tests ONE candidate row of the column (lane i: row i,
+                    // and row i + 64 in the 72-row kernels): "some u |a_ik| > |a_kk|, i > k" with the same products
+                    // and compares as the oracle's test, one ballot.  The test costs two VALU instructions instead of
+                    // a multiply, a compare and a count per row block in the owner lanes, and the division above
+                    // runs under the LDS round trip instead of after the ballot.
                     wave_lds_sync();  // the previous step's reads of colw are done before it is rewritten
                     if (owner) {
 #pragma unroll
                         for (int a = bk; a < RM; ++a) colw[ty + G * a] = R[a][bk];
-#pragma unroll
-                        for (int a = bk; a < RM; ++a) nbad += ((a > bk || ty > kk) && A.u * fabs(R[a][bk]) > aak) ? 1 : 0;
                     }
                     // publish -> read-back across lanes: explicit (see wave_lds_sync; without it the compiler may
                     // legally run the non-owners' reads before the owners' stores)
                     wave_lds_sync();
-                    // the update's operands read now, whatever the test says, so their latency can run under the
-                    // division and the ballot
+                    // rows < G * bk of colw are stale (earlier steps) but <= k: excluded by the row test.  The test's
+                    // reads go first and are unconditional (no branch, no wait for the operand reads behind them)
+                    constexpr int NR = G * RM;
+                    const double t0 = colw[NR >= 64 ? tid : (tid < NR ? tid : 0)];
+                    const double t1 = NR > 64 ? colw[64 + (tid < NR - 64 ? tid : 0)] : 0.0;
                     double lv[RM], cw[RM];
 #pragma unroll
                     for (int a = bk; a < RM; ++a) {
                         lv[a] = colw[ty + G * a];
                         cw[a] = colw[tx + G * a];
                     }
-                    need = (__ballot(nbad != 0) != 0) || !(aak > thres);
+                    // the division is computed before the ballot (not sunk into the pivot branch): it runs under the
+                    // LDS round trip
+                    double dinv = 1.0 / akk;
+                    asm volatile("" : "+v"(dinv));
+                    bool bad = (tid > k) & (tid < NR) & (A.u * fabs(t0) > aak);
+                    if constexpr (NR > 64) bad = bad | ((tid < NR - 64) & (tid + 64 > k) & (A.u * fabs(t1) > aak));
+                    need = (__ballot(bad) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange (k < 64: its |a_kk| enters minpiv after the loop)
                         double cv[RM];
