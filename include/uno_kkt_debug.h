@@ -33,8 +33,11 @@ int64_t uno_kkt_debug_front_info(uno_kkt_t handle, int32_t* front_order, int32_t
 /* Equilibration of the last factorization: the scaling s (by original index) and ||A_pre||_inf as the
  * library computed them (waits for the factorization).  Returns 0, or an error code. */
 /* option comm_trace = 1: the attached transport's calls in order, 4 int64 per record (op, peer / root, bytes,
- * reduction op; op 0 send, 1 recv, 2 allreduce, 3 broadcast, 4 group_begin, 5 group_end).  Returns the number of
- * records (-1: no traced transport); at most cap / 4 are copied; clear != 0 starts a new trace. */
+ * reduction op; op 0 send, 1 recv, 2 allreduce, 3 broadcast, 4 group_begin, 5 group_end, 6 order: recorded right
+ * before every send / recv / collective with peer = 1 when the call is enqueued on the handle's main stream and
+ * bytes = the bit mask of side streams holding factor launches not yet joined into it -- 1 / 0 is the stream
+ * ordering after every producing launch).  Returns the number of records (-1: no traced transport); at most
+ * cap / 4 are copied; clear != 0 starts a new trace. */
 int64_t uno_kkt_debug_comm_trace(uno_kkt_t handle, int64_t* out, int64_t cap, int clear);
 int uno_kkt_debug_scaling(uno_kkt_t handle, double* scale, double* anorm);
 #ifdef __cplusplus

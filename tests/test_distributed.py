@@ -225,6 +225,15 @@ def check_comm_traces(traces):
     operation, broadcast size and root) are issued in the same order with the same arguments on every rank."""
     world = len(traces)
     coll = []
+    # stream ordering (VERDICT r5 item 8): every send / recv / collective is enqueued on the handle's main stream
+    # with no side-stream factor launch left un-joined into it, i.e. after every launch that produced its buffer
+    for q, tr in enumerate(traces):
+        for i, t in enumerate(tr):
+            if t[0] in ("send", "recv", "allreduce", "broadcast"):
+                assert i > 0 and tr[i - 1][0] == "order", f"rank {q}: {t[0]} #{i} without an order record"
+                assert tr[i - 1][1] == 1, f"rank {q}: {t[0]} #{i} not on the main stream"
+                assert tr[i - 1][2] == 0, f"rank {q}: {t[0]} #{i} enqueued before side-stream launches were joined"
+    traces = [[t for t in tr if t[0] != "order"] for tr in traces]
     for q, tr in enumerate(traces):
         depth = 0
         for op, peer, nbytes, red in tr:
@@ -417,13 +426,18 @@ def test_gate_agrees_across_ranks(ua):
 
 def test_comm_trace_checker_catches_mismatches():
     """The RCCL-program checker of test_multiprocess_rccl_call_sequence rejects a size mismatch, a send outside
-    a group and diverging collectives (CPU only: synthetic traces)."""
-    good = [[("group_begin", -1, 0, -1), ("send", 1, 64, -1), ("group_end", -1, 0, -1), ("allreduce", -1, 24, 0)],
-            [("group_begin", -1, 0, -1), ("recv", 0, 64, -1), ("group_end", -1, 0, -1), ("allreduce", -1, 24, 0)]]
+    a group, diverging collectives, and an exchange enqueued off the main stream or before a side stream's factor
+    launches were joined (CPU only: synthetic traces)."""
+    O = ("order", 1, 0, -1)
+    good = [[("group_begin", -1, 0, -1), O, ("send", 1, 64, -1), ("group_end", -1, 0, -1), O, ("allreduce", -1, 24, 0)],
+            [("group_begin", -1, 0, -1), O, ("recv", 0, 64, -1), ("group_end", -1, 0, -1), O, ("allreduce", -1, 24, 0)]]
     assert check_comm_traces(good) == (1, 1)
     bad_size = [good[0], [t if t[0] != "recv" else ("recv", 0, 56, -1) for t in good[1]]]
     bad_group = [[t for t in good[0] if t[0] != "group_begin" and t[0] != "group_end"], good[1]]
     bad_coll = [good[0], good[1][:-1] + [("allreduce", -1, 24, 1)]]
-    for bad in (bad_size, bad_group, bad_coll):
+    bad_stream = [[("order", 0, 0, -1) if i == 1 else t for i, t in enumerate(good[0])], good[1]]
+    bad_join = [good[0], [("order", 1, 1, -1) if i == 4 else t for i, t in enumerate(good[1])]]
+    bad_missing = [[t for i, t in enumerate(good[0]) if i != 1], good[1]]
+    for bad in (bad_size, bad_group, bad_coll, bad_stream, bad_join, bad_missing):
         with pytest.raises(AssertionError):
             check_comm_traces(bad)

@@ -54,8 +54,9 @@ def both(n, r, c, v, **opt):
     return g, o
 
 
+@pytest.mark.parametrize("pack", [1, 0])
 @pytest.mark.parametrize("case", ["c2", "random", "hub"])
-def test_scaling_bit_identical(uno_amd, case):
+def test_scaling_bit_identical(uno_amd, case, pack):
     """The equilibration (ICNTL(8)=8 restated as 3 symmetric infinity-norm sweeps, MUMPSSolver.cpp:82) is
     the oracle's to the bit: every scaling factor equal, and ||A_pre||_inf (whose summation order differs)
     within 1e-14 relative, so the null-pivot threshold eps * 1e-5 * ||A_pre||_inf is the oracle's."""
@@ -68,7 +69,7 @@ def test_scaling_bit_identical(uno_amd, case):
     else:
         rr, cc, vv, _ = random_sym(np.random.default_rng(5), 60, 0.3, zero_diag_frac=0.5)
         n, r, c, v = 60, rr, cc, vv * np.exp(np.random.default_rng(6).uniform(-20, 20, len(vv)))
-    g, o = both(n, r, c, v)
+    g, o = both(n, r, c, v, sweep_pack=pack)  # pack 0: the flat k_pack before the sweeps (option sweep_pack)
     sg, anorm = g.debug_scaling()
     so, thres = o.scaling()
     assert np.isfinite(sg).all() and (sg > 0).all()
@@ -230,6 +231,34 @@ def test_dataflow_solve_kernels_bit_identical(uno_amd, rg):
     assert gd.inertia() == gl.inertia()
     np.testing.assert_array_equal(gd.solve(b), gl.solve(b))
     assert gd.stats()["solve_aborts"] == 0
+
+
+@pytest.mark.parametrize("levels", [1, 2, 3])
+def test_forward_flat_levels_bit_identical(uno_amd, levels):
+    """Round 6: the walks' bottom levels as flat launches (k_solve_fwd_flat before the forward walk, k_solve_bwd_flat
+    after the backward walk, one per level;
+    option solve_flat_levels, default 2) give solutions bit-identical to the walk that solves every front itself
+    (solve_flat_levels = 0), over repeated solves, in the plugin's relaxed mode, and after a refactorization; the
+    walk's fronts then wait only for their walk children."""
+    from uno_amd import arrowband, SEEDS, HipKKT
+    n, nv, m, r, c, v, b = arrowband(100000, SEEDS["C3"])
+    gl = HipKKT(0, solve_flat_levels=levels, delay_relaxed=0)
+    gw = HipKKT(0, solve_flat_levels=0, delay_relaxed=0)
+    for g in (gl, gw):
+        g.analyze(n, r, c)
+        g.factorize(v)
+    assert gl.inertia() == gw.inertia()
+    for rep in range(3):
+        np.testing.assert_array_equal(gl.solve(b * (rep + 1)), gw.solve(b * (rep + 1)))
+    v2 = np.array(v)
+    v2[:n] -= 0.25
+    for g in (gl, gw):
+        g.factorize(v2)
+    assert gl.inertia() == gw.inertia()
+    xl = gl.solve(b)
+    np.testing.assert_array_equal(xl, gw.solve(b))
+    assert rel_residual(n, r, c, v2, xl, b) < RES_TOL
+    assert gl.stats()["solve_aborts"] == 0 and gw.stats()["solve_aborts"] == 0
 
 
 def test_arrowband_c2(uno_amd):

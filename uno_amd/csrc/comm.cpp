@@ -301,24 +301,34 @@ public:
     hipError_t group_begin() override { rec(4, -1, 0, -1); return in_->group_begin(); }
     hipError_t group_end() override { rec(5, -1, 0, -1); return in_->group_end(); }
     hipError_t send(const void* buf, size_t bytes, int peer, hipStream_t s) override {
+        order(s);
         rec(0, peer, bytes, -1);
         return in_->send(buf, bytes, peer, s);
     }
     hipError_t recv(void* buf, size_t bytes, int peer, hipStream_t s) override {
+        order(s);
         rec(1, peer, bytes, -1);
         return in_->recv(buf, bytes, peer, s);
     }
     hipError_t allreduce(void* buf, size_t count, RedOp op, hipStream_t s) override {
+        order(s);
         rec(2, -1, count * 8, (int)op);
         return in_->allreduce(buf, count, op, s);
     }
     hipError_t broadcast(void* buf, size_t bytes, int root, hipStream_t s) override {
+        order(s);
         rec(3, root, bytes, -1);
         return in_->broadcast(buf, bytes, root, s);
     }
     std::vector<int64_t> log;
+    std::function<std::pair<int, int>(hipStream_t)> probe;
 
 private:
+    void order(hipStream_t s) {
+        if (!probe) return;
+        const std::pair<int, int> o = probe(s);
+        rec(6, o.first, (size_t)o.second, -1);
+    }
     void rec(int op, int peer, size_t bytes, int red) {
         log.push_back(op);
         log.push_back(peer);
@@ -330,6 +340,10 @@ private:
 }  // namespace
 
 Transport* make_tracing_transport(Transport* inner) { return inner ? new TracingTransport(inner) : nullptr; }
+
+void comm_trace_set_probe(Transport* t, std::function<std::pair<int, int>(hipStream_t)> probe) {
+    if (auto* tt = dynamic_cast<TracingTransport*>(t)) tt->probe = std::move(probe);
+}
 
 bool comm_trace_records(Transport* t, std::vector<int64_t>& out, bool clear) {
     auto* tt = dynamic_cast<TracingTransport*>(t);

@@ -17,7 +17,9 @@
 
 #include <cstddef>
 #include <cstdint>
+#include <functional>
 #include <string>
+#include <utility>
 #include <vector>
 
 namespace ukkt {
@@ -68,6 +70,11 @@ Transport* make_host_transport(const HostComm& cb, int rank, int world);
 // host or local transport is the sequence the RCCL transport would see (ncclSend / ncclRecv sizes, peers,
 // grouping, collective order).
 Transport* make_tracing_transport(Transport* inner);
+// stream-order probe of a tracing transport: called with the stream of every send / recv / collective, it returns
+// (the call is on the handle's main stream, the side streams whose launches are not yet joined into it as a bit
+// mask); the transport records it as an op 6 record (peer = on-main flag, bytes = mask) right before the call.  An
+// exchange is ordered after every producing launch iff it is on the main stream with mask 0.
+void comm_trace_set_probe(Transport* t, std::function<std::pair<int, int>(hipStream_t)> probe);
 // the records of a tracing transport (empty for any other transport); clear: start a new trace
 bool comm_trace_records(Transport* t, std::vector<int64_t>& out, bool clear);
 

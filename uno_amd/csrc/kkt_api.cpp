@@ -198,6 +198,8 @@ struct uno_kkt {
     DBuf<unsigned long long> df_abort64;
     int df_grid = 0, df_lds = 0;   // 0 grid: not eligible -> level schedule
     int solve_rg = 1;              // option "solve_rg": register-resident forward walk kernel (k_solve_fwd_rg)
+    int solve_flat = 0;            // option "solve_flat_levels": the walks' bottom levels as flat launches (measured
+                                   // slower than the walks at C3, DESIGN.md section 4 round 6: off by default)
     int solve_rg_bwd = 0;          // option "solve_rg_bwd": register-resident backward walk (k_solve_bwd_rg; its
                                    // transpose-reduced rectangle sums in another order, so the level schedule follows)
     int rg_grid_f = 0, rg_grid_b = 0;
@@ -216,6 +218,11 @@ struct uno_kkt {
                                           // contribution row, -1: not in the walk (k_xpos)
     DBuf<int32_t> rg_desc, ov_desc;  // register kernels: the walk split into p <= 32, m <= 72 fronts and the others
     int32_t rg_nf = 0, ov_nf = 0, ov_grid = 0;
+    DBuf<int32_t> rgf_desc, flat_desc;  // forward: rg_desc without its flat levels, and those (k_solve_fwd_flat)
+    DBuf<int32_t> bwd_desc;             // backward LDS-panel walk: df_desc without the flat levels (k_solve_bwd_flat)
+    int32_t bwd_nf = 0;
+    int32_t rgf_nf = 0;
+    std::vector<int32_t> flat_off;      // flat_desc positions of each flat level (flat_off.size() - 1 launches)
     DBuf<int64_t> df_cvx_off, df_ch_cvx_off, df_xs_off;
     DBuf<uint32_t> df_cnt, df_done, df_abort;
     DBuf<double> df_cvx, df_xs;
@@ -272,6 +279,7 @@ struct uno_kkt {
     DBuf<unsigned long long> omega_d;
     int resid_fronts = 1;                 // option: refinement residual over the fronts' slots (launch_resid)
     int sweep_reset = 1;                  // option: the first sweep resets the counters (no k_reset_counters)
+    int sweep_pack = 1;                   // option: the COO -> slot pack fused into the first sweep (0: flat k_pack first)
     int64_t resid_long = kResidShort;     // option (tests): rows with more partials are summed by chunks
     int rz_state = 0;                     // 0: index not built, 1: built, -1: not applicable (old symv)
     DBuf<int32_t> rz_ptr, rz_pos, rz_long, rz_chunk_off, rz_chunk_row;
@@ -292,6 +300,8 @@ struct uno_kkt {
     double dist_min_eff = 0.5;    // option dist_min_efficiency
     int dist_force = 0;           // option dist_force: partition whatever the estimate (tests, experiments)
     int comm_trace = 0;           // option comm_trace: the transport records its calls (uno_kkt_debug_comm_trace)
+    int side_pending = 0;         // side streams (bit 0: stream3, bit 1: stream4) with factor launches not yet joined
+                                  // into `stream` (the comm trace's order records check it is 0 at every exchange)
     int gather_solution = 1;
     DistState dist;
     uno_kkt_stats_t st{};
@@ -309,6 +319,12 @@ namespace {
 int set_err(uno_kkt_t h, int code, const std::string& msg) {
     if (h) h->err = msg;
     return code;
+}
+
+// comm trace (tests): every exchange records whether it is enqueued on the main stream after every producing
+// launch -- the RCCL call is stream-ordered, so that is what makes its buffer the finished one
+void install_order_probe(uno_kkt_t h) {
+    ukkt::comm_trace_set_probe(h->comm, [h](hipStream_t s) { return std::make_pair(s == h->stream ? 1 : 0, h->side_pending); });
 }
 
 // hipHostUnregister of the caller's page-locked buffer (option pin_host_values) waits for every copy that
@@ -434,6 +450,9 @@ DfArgs dataflow_args(uno_kkt_t h) {
     D.stamps = h->want_solve_stamps ? h->df_stamps.p : nullptr;
     D.rg_desc = h->rg_desc.p; D.rg_nf = h->rg_nf;
     D.ov_desc = h->ov_desc.p; D.ov_nf = h->ov_nf; D.ov_grid = h->ov_grid;
+    D.rgf_desc = h->rgf_desc.p; D.rgf_nf = h->rgf_nf;
+    D.flat_desc = h->flat_desc.p;
+    D.bdesc = h->bwd_desc.p; D.bnf = h->bwd_nf;
     return D;
 }
 
@@ -1026,8 +1045,9 @@ void set_rg_grids(uno_kkt_t h) {
     h->ov_grid = std::min(h->ov_nf, 32);
     for (int d = 0; d < 2; ++d) {
         const int resident = solve_rg_grid(d == 0, 1 << 30, h->rg_wpe);
-        int g = std::min(resident, h->rg_nf + h->ov_grid);
-        if (resident <= h->ov_grid || (h->rg_nf > 0 && g - h->ov_grid < 1)) g = 0;  // no room: df kernels
+        const int nwalk = d == 0 ? h->rgf_nf : h->rg_nf;  // the forward walk leaves its leaves to k_solve_fwd_leaf
+        int g = std::min(resident, nwalk + h->ov_grid);
+        if (resident <= h->ov_grid || (nwalk > 0 && g - h->ov_grid < 1)) g = 0;  // no room: df kernels
         (d == 0 ? h->rg_grid_f : h->rg_grid_b) = g;
     }
 }
@@ -1099,15 +1119,33 @@ hipError_t setup_dataflow(uno_kkt_t h) {
     {
         std::vector<int32_t> desc(walk.size() * 16, 0);
         auto put64 = [&](int32_t* d, int64_t v) { d[0] = (int32_t)(uint32_t)v; d[1] = (int32_t)(uint32_t)((uint64_t)v >> 32); };
+        // the bottom solve_flat levels of the register class go to k_solve_fwd_flat (one flat launch per level
+        // before the forward walk): a front is flat when its level is < solve_flat, it fits the register kernels
+        // and all its children are flat -- unless the walk would then be empty (tiny systems); kDescNW counts the
+        // children a walk front waits for
+        std::vector<char> leaf(S.nf, 0);  // flat
+        int64_t nleaf = 0, nrg = 0;
+        for (int32_t f : walk) {  // children before parents
+            const bool rg = S.f_p[f] <= 32 && S.f_m[f] <= 72;
+            nrg += rg;
+            bool ok = rg && S.f_level[f] < h->solve_flat;
+            for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1] && ok; ++q) ok = leaf[S.child[q]] != 0;
+            if (ok) { leaf[f] = 1; ++nleaf; }
+        }
+        if (nleaf == nrg) std::fill(leaf.begin(), leaf.end(), 0);
         for (size_t t = 0; t < walk.size(); ++t) {
             const int32_t f = walk[t];
             int32_t* d = desc.data() + 16 * t;
             d[kDescF] = f; d[kDescM] = S.f_m[f]; d[kDescP] = S.f_p[f]; d[kDescPar] = S.f_parent[f];
             d[kDescC0] = S.f_child_off[f]; d[kDescC1] = S.f_child_off[f + 1];
+            int nw = 0;
+            for (int q = S.f_child_off[f]; q < S.f_child_off[f + 1]; ++q) nw += !leaf[S.child[q]];
+            d[kDescNW] = nw;
             put64(d + kDescRo, S.f_rows_off[f]); put64(d + kDescLo, S.f_L_off[f]);
             put64(d + kDescCvx, cvx[f]); put64(d + kDescXs, xs[f]);
         }
         if ((e = h->df_desc.upload(desc, s)) != hipSuccess) return e;
+        std::vector<int32_t> bwd;  // filled below with the flat set (the backward walk without the flat levels)
         // the register kernels' two walks (same order): p <= 32, m <= 72 fronts, and the rest
         std::vector<int32_t> rgd, ovd;
         for (size_t t = 0; t < walk.size(); ++t) {
@@ -1115,12 +1153,33 @@ hipError_t setup_dataflow(uno_kkt_t h) {
             auto& dst = (S.f_p[f] <= 32 && S.f_m[f] <= 72) ? rgd : ovd;
             dst.insert(dst.end(), desc.begin() + 16 * t, desc.begin() + 16 * (t + 1));
         }
+        std::vector<int32_t> rgf, lfd;  // the forward register walk without the flat levels, and those by level
+        h->flat_off.assign(1, 0);
+        for (int lev = 0; lev < h->solve_flat; ++lev) {
+            for (size_t t = 0; t < rgd.size() / 16; ++t) {
+                const int32_t f = rgd[16 * t + kDescF];
+                if (leaf[f] && S.f_level[f] == lev) lfd.insert(lfd.end(), rgd.begin() + 16 * t, rgd.begin() + 16 * (t + 1));
+            }
+            h->flat_off.push_back((int32_t)(lfd.size() / 16));
+        }
+        for (size_t t = 0; t < rgd.size() / 16; ++t)
+            if (!leaf[rgd[16 * t + kDescF]]) rgf.insert(rgf.end(), rgd.begin() + 16 * t, rgd.begin() + 16 * (t + 1));
         h->rg_nf = (int32_t)(rgd.size() / 16);
         h->ov_nf = (int32_t)(ovd.size() / 16);
+        h->rgf_nf = (int32_t)(rgf.size() / 16);
         if (rgd.empty()) rgd.assign(16, 0);
         if (ovd.empty()) ovd.assign(16, 0);
+        if (rgf.empty()) rgf.assign(16, 0);
+        if (lfd.empty()) lfd.assign(16, 0);
         if ((e = h->rg_desc.upload(rgd, s)) != hipSuccess) return e;
         if ((e = h->ov_desc.upload(ovd, s)) != hipSuccess) return e;
+        if ((e = h->rgf_desc.upload(rgf, s)) != hipSuccess) return e;
+        if ((e = h->flat_desc.upload(lfd, s)) != hipSuccess) return e;
+        for (size_t t = 0; t < desc.size() / 16; ++t)
+            if (!leaf[desc[16 * t + kDescF]]) bwd.insert(bwd.end(), desc.begin() + 16 * t, desc.begin() + 16 * (t + 1));
+        h->bwd_nf = (int32_t)(bwd.size() / 16);
+        if (bwd.empty()) bwd.assign(16, 0);
+        if ((e = h->bwd_desc.upload(bwd, s)) != hipSuccess) return e;
     }
     if ((e = h->df_cvx_off.upload(cvx, s)) != hipSuccess) return e;
     if ((e = h->df_ch_cvx_off.upload(chx, s)) != hipSuccess) return e;
@@ -1416,9 +1475,11 @@ int enqueue_factorization(uno_kkt_t h) {
     Symbolic& S = h->S;
     hipStream_t s = h->stream;
     // counters, minbits, anorm: reset by the first equilibration sweep when it runs (no launch of its own)
-    const bool reset_in_sweep = h->use_front_sweeps && S.nf > 0 && h->sweep_reset;
+    // the pack fused into the first sweep (option sweep_pack, one GPU, scaling on), else the flat k_pack grid
+    const bool fused_pack = h->use_front_sweeps && (h->sweep_pack || h->world != 1 || h->scale_iters <= 0);
+    const bool reset_in_sweep = fused_pack && S.nf > 0 && h->sweep_reset;
     if (!reset_in_sweep) HIPCHK(h, launch_reset_counters(h->counters.p, s));
-    if (h->use_front_sweeps) {
+    if (fused_pack) {
         // k_pack runs inside launch_front_sweeps (timed with the scaling)
     } else {
         TimerScope t(h, KC_PACK);
@@ -1461,7 +1522,7 @@ int enqueue_factorization(uno_kkt_t h) {
             W.flong = h->n_long > 0 ? h->flong.p : nullptr;
             W.rmax_zero = h->rmaxk_clean;
             W.counters = reset_in_sweep ? h->counters.p : nullptr;
-            HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s));
+            HIPCHK(h, launch_front_sweeps(W, h->scale_iters, s, fused_pack));
             h->rmaxk_clean = true;  // k_sweep_final cleared it
             if (h->overlap_norm && !h->exact_next) {
                 h->last_optimistic = true;  // row sums only if a pivot is small (sync_and_verify)
@@ -1523,6 +1584,7 @@ int enqueue_factorization(uno_kkt_t h) {
     bool split = false;  // stream3 holds launches of the previous level not yet joined into s
     auto join3 = [&]() -> hipError_t {
         hipError_t e = hipEventRecord(h->ev_join, h->stream3);
+        if (e == hipSuccess) h->side_pending &= ~1;
         return e == hipSuccess ? hipStreamWaitEvent(s, h->ev_join, 0) : e;
     };
     for (size_t q = 0; q < lp.fac.size();) {
@@ -1536,6 +1598,7 @@ int enqueue_factorization(uno_kkt_t h) {
             HIPCHK(h, hipEventRecord(h->ev_join, h->stream3));
             HIPCHK(h, hipStreamWaitEvent(s, h->ev_join, 0));
             HIPCHK(h, hipStreamWaitEvent(h->stream3, h->ev_fork, 0));
+            h->side_pending &= ~1;
         } else {
             if (split) HIPCHK(h, join3());
             if (multi) {
@@ -1555,6 +1618,8 @@ int enqueue_factorization(uno_kkt_t h) {
             if (h->concurrent_classes == 2) ls = u > q ? h->stream3 : s;
             else if (three) ls = (u - q) % 3 == 0 ? s : ((u - q) % 3 == 1 ? h->stream3 : h->stream4);
             else if (h->concurrent_classes) ls = ((u - q) & 1) ? h->stream3 : s;
+            if (ls == h->stream3) h->side_pending |= 1;
+            if (ls == h->stream4) h->side_pending |= 2;
             if (L.global) {
                 const int rc = run_big_fronts(h, A, lp.fac_fronts.p + L.begin, L, ls);
                 if (rc != UNO_KKT_OK) return rc;
@@ -1568,6 +1633,7 @@ int enqueue_factorization(uno_kkt_t h) {
             HIPCHK(h, join3());
             HIPCHK(h, hipEventRecord(h->ev_join4, h->stream4));
             HIPCHK(h, hipStreamWaitEvent(s, h->ev_join4, 0));
+            h->side_pending &= ~2;
         }
         q = r;
     }
@@ -1717,6 +1783,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "refine") h->refine = std::max(0, (int)value);
     else if (n == "refine_tol") h->refine_tol = std::max(0.0, value);
     else if (n == "sweep_reset") h->sweep_reset = value != 0.0;
+    else if (n == "sweep_pack") h->sweep_pack = value != 0.0;
     else if (n == "cbpos") h->cbpos_opt = value != 0.0;  // takes effect at the next analysis
     else if (n == "resid_fronts") { h->resid_fronts = value != 0.0; h->rz_state = 0; }
     else if (n == "resid_long") { h->resid_long = std::max<int64_t>(1, (int64_t)value); h->rz_state = 0; }
@@ -1739,8 +1806,10 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "comm_trace") {  // record the transport calls (tests): wraps the attached transport, if any
         h->comm_trace = value != 0.0;
         std::vector<int64_t> dummy;
-        if (h->comm_trace && h->comm && !ukkt::comm_trace_records(h->comm, dummy, false))
+        if (h->comm_trace && h->comm && !ukkt::comm_trace_records(h->comm, dummy, false)) {
             h->comm = ukkt::make_tracing_transport(h->comm);
+            install_order_probe(h);
+        }
     }
     else if (n == "dataflow_factor") {
         h->dff_enabled = std::max(0, std::min(2, (int)value));
@@ -1763,8 +1832,9 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
             HIPCHK(h, hipStreamSynchronize(h->stream));
         }
     }
-    else if (n == "solve_rg" || n == "solve_rg_bwd") {
-        (n == "solve_rg" ? h->solve_rg : h->solve_rg_bwd) = value != 0.0;
+    else if (n == "solve_rg" || n == "solve_rg_bwd" || n == "solve_flat_levels") {
+        if (n == "solve_flat_levels") h->solve_flat = std::max(0, (int)value);
+        else (n == "solve_rg" ? h->solve_rg : h->solve_rg_bwd) = value != 0.0;
         if (h->analyzed) {
             HIPCHK(h, setup_dataflow(h));
             HIPCHK(h, hipStreamSynchronize(h->stream));
@@ -2055,8 +2125,21 @@ int solve_core(uno_kkt_t h, const double* b, double* xd, bool allow_df = true, b
     DfArgs Df;
     auto walk = [&](bool forward) -> hipError_t {
         const int g = forward ? h->rg_grid_f : h->rg_grid_b;
-        if ((forward ? h->solve_rg != 0 : h->new_bwd) && g > 0) return launch_solve_rg(A, Df, g, forward, h->rg_wpe, s);
-        return launch_solve_df(A, Df, h->df_grid, h->df_lds, forward, s);
+        if ((forward ? h->solve_rg != 0 : h->new_bwd) && g > 0) {
+            if (forward) {  // the flat levels first, level by level (no counters), then the walk of the rest
+                for (size_t l = 0; l + 1 < h->flat_off.size(); ++l) {
+                    const hipError_t e = launch_solve_fwd_flat(A, Df, h->flat_off[l], h->flat_off[l + 1] - h->flat_off[l], s);
+                    if (e != hipSuccess) return e;
+                }
+            }
+            return launch_solve_rg(A, Df, g, forward, h->rg_wpe, s);
+        }
+        if (forward) return launch_solve_df(A, Df, h->df_grid, h->df_lds, true, s);  // every front (no flat launches)
+        // backward: the walk without the flat levels, then those level by level, top level first
+        hipError_t e = launch_solve_df(A, Df, h->df_grid, h->df_lds, false, s);
+        for (size_t l = h->flat_off.size(); e == hipSuccess && l-- > 1;)
+            e = launch_solve_bwd_flat(A, Df, h->flat_off[l - 1], h->flat_off[l] - h->flat_off[l - 1], h->df_lds, s);
+        return e;
     };
     if (df) {
         Df = dataflow_args(h);
@@ -2708,6 +2791,7 @@ int uno_kkt_comm_unique_id(unsigned char id[128]) {
 static int attach(uno_kkt_t h, ukkt::Transport* t) {
     delete h->comm;
     h->comm = h->comm_trace ? ukkt::make_tracing_transport(t) : t;
+    if (h->comm_trace) install_order_probe(h);
     h->own_device = false;
     h->rank = h->comm_rank = t->rank();
     h->world = h->comm_world = t->size();

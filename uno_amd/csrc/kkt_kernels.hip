@@ -2539,6 +2539,7 @@ __device__ __forceinline__ int bwd_chunk_begin(int m, int p, int c1, int win) {
 constexpr int kPre = 8;  // 1 024 doubles: the default panel window (solve_window) fits
 struct FrontRec {
     int f, m, p, sz, par, c0, c1;
+    int nw;  // children the forward walk waits for (kDescNW)
     int64_t ro, Lo;
     int64_t xoff;  // forward: cvx slot
     int64_t woff;  // xs slot (the front's pivots in elimination order)
@@ -2573,6 +2574,7 @@ __device__ __forceinline__ FrontRec df_record(int dv) {
     r.par = w(kDescPar);
     r.c0 = w(kDescC0);
     r.c1 = w(kDescC1);
+    r.nw = w(kDescNW);
     r.ro = w64(kDescRo);
     r.Lo = w64(kDescLo);
     r.xoff = w64(kDescCvx);
@@ -2981,6 +2983,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
     extern __shared__ __attribute__((aligned(16))) double smem_s[];
     const int lane = threadIdx.x;
     int t = blockIdx.x;
+    // the backward walk: the walk without its flat levels (k_solve_bwd_flat solves those after it)
+    D.desc = D.bdesc;
+    D.nf = D.bnf;
     if (t >= D.nf) return;
     FrontPre q;
     q.r = df_record(df_desc_load(D, D.nf - 1 - t));
@@ -3027,6 +3032,37 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_
         __syncthreads();
     }
     signal();
+}
+
+// Backward of the flat levels (the forward's k_solve_fwd_flat fronts), one launch per level after the backward
+// walk, top level first, one wave per front: no dependency waits (the launch boundary orders a level after the
+// walk / the level above) and no done flags (a flat front's children are flat).  The walk's per-front code
+// (df_issue, df_stage_window, bwd_compute_win): bit-identical.
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) void k_solve_bwd_flat(SolveArgs A, DfArgs D, int begin,
+                                                                                                 int count) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    const int t = blockIdx.x;
+    if (t >= count) return;
+    FrontPre q;
+    q.r = df_record(D.flat_desc[(int64_t)(begin + t) * 16 + (lane & 15)]);
+    df_issue<false>(A, D, q);
+    const int m = q.r.m, p = q.r.p;
+    unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)q.r.f + 4 : nullptr;
+    if (st && lane == 0) st[0] = st[1] = __builtin_amdgcn_s_memrealtime();
+    double* P = smem_s;
+    double* x = smem_s + D.win;
+    int32_t* ipl = (int32_t*)(smem_s + D.piv_off);
+    ipl[lane] = q.mypiv;
+    if (lane < m) x[lane] = lane < p ? q.e0 : ld_sc1(D.xs + q.a0);
+    if (lane + 64 < m) x[lane + 64] = ld_sc1(D.xs + q.a1);
+    df_stage_window(A, q, P);
+    __syncthreads();
+    if (st && lane == 0) st[2] = __builtin_amdgcn_s_memrealtime();
+    const int mypiv = ipl[lane];
+    const double xj = bwd_compute_win(A.L, q.r.Lo, m, p, P, D.win, q.kw, x, mypiv);
+    if (lane < p) st_sc1(D.xs + q.r.woff + lane, xj);
+    if (st && lane == 0) st[3] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---- register-resident dataflow solve (round 4): the default dataflow kernels ----
@@ -3082,7 +3118,7 @@ __device__ void rg_fwd_over(const SolveArgs& A, const DfArgs& D, const FrontRec&
     fpl[lane] = lane < m ? A.fpos[ro + lane] : 0;
     fpl[lane + 64] = lane + 64 < m ? A.fpos[ro + lane + 64] : 0;
     if (r.c1 > r.c0) {
-        df_wait(D.cnt + f, D.epoch * (uint32_t)(r.c1 - r.c0), D.abort_flag);
+        if (r.nw > 0) df_wait(D.cnt + f, D.epoch * (uint32_t)r.nw, D.abort_flag);
         __syncthreads();
         fwd_extend_add<true>(A, D, r.c0, r.c1, my_cm, my_rmo, my_cxo, y, fpl);
     }
@@ -3248,15 +3284,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         return;
     }
     int t = blockIdx.x;
-    if (t >= D.rg_nf) return;
+    if (t >= D.rgf_nf) return;
     double* Th = smem_s + 192;                   // 8 x 33 doubles: rows 64..71 of the panel
-    const int* desc = D.rg_desc;
+    const int* desc = D.rgf_desc;
     FrontRec r = df_record(desc[t * 16 + (lane & 15)]);
     RgFwdMeta q;
     double B[kRgCols];
     rg_fwd_meta(A, D, r, q);
     rg_load_cols(A.L, r.Lo, r.m, r.p, 0, 0, B);
-    int dn = desc[min(t + G, D.rg_nf - 1) * 16 + (lane & 15)];
+    int dn = desc[min(t + G, D.rgf_nf - 1) * 16 + (lane & 15)];
     for (;;) {
         const int m = r.m, p = r.p, f = r.f, par = r.par;
         const int64_t xoff = r.xoff, woff = r.woff;
@@ -3277,8 +3313,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         fpl[lane] = q.fp0;
         fpl[lane + 64] = q.fp1;
         if (r.c1 > r.c0) {
-            const uint32_t target = D.epoch * (uint32_t)(r.c1 - r.c0);
-            if ((int32_t)(q.dep - target) < 0) df_wait(D.cnt + f, target, D.abort_flag);
+            const uint32_t target = D.epoch * (uint32_t)r.nw;  // leaves solved before the walk are not waited for
+            if (r.nw > 0 && (int32_t)(q.dep - target) < 0) df_wait(D.cnt + f, target, D.abort_flag);
             rg_extend_add(A, D, r.c0, r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
         }
         wave_lds_sync();  // y, fpl and Th were written by other lanes
@@ -3286,12 +3322,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         double a1 = m > 64 ? y[lane + 64] : 0.0;
         if (st && lane == 0) st[1] = __builtin_amdgcn_s_memrealtime();
         const int tn = t + G;
-        const bool more = tn < D.rg_nf;
+        const bool more = tn < D.rgf_nf;
         FrontRec rn = r;
         asm volatile("" ::: "memory");  // the next front's loads stay below this front's assembly
         if (more) {
             rn = df_record(dn);
-            dn = desc[min(tn + G, D.rg_nf - 1) * 16 + (lane & 15)];
+            dn = desc[min(tn + G, D.rgf_nf - 1) * 16 + (lane & 15)];
             rg_fwd_meta(A, D, rn, q);
         } else {
             rn.p = 0;
@@ -3355,6 +3391,95 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         r = rn;
         t = tn;
     }
+}
+
+// Forward of the bottom levels of the register walk (option solve_flat_levels, default 2: levels 0 and 1), one
+// flat launch per level before the walk, one wave per front.  The walk spends most of such a front's time issuing
+// and draining loads one front after the other (its drain before the parent's counter also waits for the next
+// front's prefetch: one vmcnt for loads and stores); here the hardware keeps as many independent fronts in flight
+// as fit, with no counters at all: the launch boundary orders a level after the one below, and the walk's
+// fronts wait only for their walk children (kDescNW).  The per-lane arithmetic is the walk's (same extend-add,
+// same steps, same order): bit-identical.  (A resident grid looping over the fronts measured slower, 72.6 vs
+// 49.3 us for the leaves at C3: its wait for the next record also waited for the finished front's stores.)
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_solve_fwd_flat(SolveArgs A, DfArgs D, int begin,
+                                                                                                   int count) {
+    extern __shared__ __attribute__((aligned(16))) double smem_s[];
+    const int lane = threadIdx.x;
+    const int t = blockIdx.x;
+    if (t >= count) return;
+    double* y = smem_s;                       // 128 doubles: the front's rows (pivoted order)
+    int32_t* fpl = (int32_t*)(smem_s + 128);  // 128 words
+    double* Th = smem_s + 192;                // 8 x 33 doubles: rows 64..71 of the panel
+    const FrontRec r = df_record(D.flat_desc[(int64_t)(begin + t) * 16 + (lane & 15)]);
+    const int m = r.m, p = r.p;
+    unsigned long long* st = D.stamps ? D.stamps + 8 * (int64_t)r.f : nullptr;
+    if (st && lane == 0) st[0] = st[1] = __builtin_amdgcn_s_memrealtime();
+    RgFwdMeta q;
+    double B[kRgCols];
+    rg_fwd_meta(A, D, r, q);
+    rg_load_cols(A.L, r.Lo, m, p, 0, 0, B);
+    const unsigned long long liveM = __ballot(lane < p && q.piv != PIV_NULL);
+    const unsigned long long twoAM = __ballot(lane < p && q.piv == PIV_2X2_A);
+    if (m > 64) {  // uniform
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+            if (8 * c < p) Th[(lane & 7) * 33 + 8 * c + (lane >> 3)] = q.H[c];
+    }
+    double y0, a1;
+    if (r.c1 > r.c0) {  // children (a lower flat level, complete): their update vectors into y, as the walk
+        y[lane] = q.e0;
+        y[lane + 64] = 0.0;
+        fpl[lane] = q.fp0;
+        fpl[lane + 64] = q.fp1;
+        rg_extend_add(A, D, r.c0, r.c1, q.my_cm, q.my_rmo, q.my_cxo, y, fpl);
+        wave_lds_sync();  // y, fpl and Th were written by other lanes
+        y0 = y[lane];
+        a1 = m > 64 ? y[lane + 64] : 0.0;
+    } else {  // a leaf: y = the right-hand side at the pivots, 0 on the contribution rows
+        wave_lds_sync();  // Th was written by other lanes
+        y0 = q.e0;
+        a1 = 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < kRgCols; ++u) {
+        if (u < p) {  // uniform
+            const double yb = readlane_d(y0, u);
+            const double yk = (liveM >> u) & 1 ? yb : 0.0;
+            const int lim = (twoAM >> u) & 1 ? u + 1 : u;
+            const double tv = y0 - B[u] * yk;
+            y0 = lane > lim ? tv : y0;
+        }
+    }
+    if (m > 64) {
+        const double ybv = lane < p && ((liveM >> lane) & 1) ? y0 : 0.0;
+        const int rw = lane < 8 ? lane : 0;
+#pragma unroll
+        for (int k = 0; k < kRgCols; ++k)
+            if (k < p) a1 -= Th[rw * 33 + k] * readlane_d(ybv, k);
+    }
+    double* cvo = D.cvx + r.xoff;
+    if (lane >= p && lane < m) st_sc1(cvo + (lane - p), y0);
+    if (lane + 64 < m) st_sc1(cvo + (lane + 64 - p), a1);
+    {
+        const double dg = q.dgl, sb = q.sbl;
+        const double dgn = __shfl(dg, lane < 63 ? lane + 1 : lane), sbn = __shfl(sb, lane < 63 ? lane + 1 : lane);
+        const double dgp = __shfl(dg, lane > 0 ? lane - 1 : 0);
+        const double yn = __shfl(y0, lane < 63 ? lane + 1 : lane), yp = __shfl(y0, lane > 0 ? lane - 1 : 0);
+        const int kind = q.piv;
+        double out = 0.0;  // null pivot contributes 0
+        if (kind == PIV_1X1) {
+            out = y0 / dg;
+        } else if (kind == PIV_2X2_A || kind == PIV_2X2_B) {
+            const bool first = kind == PIV_2X2_A;
+            const double a = first ? dg : dgp, b = first ? sbn : sb, e = first ? dgn : dg;
+            const double det = a * e - b * b;
+            const double yA = first ? y0 : yp, yB = first ? yn : y0;
+            out = first ? (e * yA - b * yB) / det : (a * yB - b * yA) / det;
+        }
+        if (lane < p) D.xs[r.woff + lane] = out;
+    }
+    if (st && lane == 0) st[2] = st[3] = __builtin_amdgcn_s_memrealtime();
 }
 
 // ---- register-resident backward (fronts with p <= 32, m <= 72) ----
@@ -4457,7 +4582,7 @@ static hipError_t launch_rowscanR(const ScanArgs& A, hipStream_t s) {
 // iters sweeps over the row-major copy.  The scalings live in the new numbering in A.scale_in / A.scale_out
 // (two scratch buffers of n doubles, the last sweep writes A.scale_out); A.scale (by original id) receives
 // the final one.
-hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
+hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s, bool fused_pack) {
     if (A0.n == 0) return hipSuccess;
     SweepArgs A = A0;
     const size_t sh = 16 * (size_t)std::max(A.max_m, 1);
@@ -4465,17 +4590,19 @@ hipError_t launch_front_sweeps(const SweepArgs& A0, int iters, hipStream_t s) {
     const int passes = iters > 0 ? iters : 1;  // iters == 0: one pass packs the values (scaling 1)
     hipError_t e = A.rmax_zero ? hipSuccess : hipMemsetAsync(A.rmax_all, 0, sizeof(unsigned long long) * A.n * passes, s);
     if (e != hipSuccess) return e;
-    // the COO values are packed into the slots by the first sweep (k_sweep_front<true, .>)
+    // the COO values are packed into the slots by the first sweep (k_sweep_front<true, .>), or by k_pack before
+    // (fused_pack false: the first sweep then reads the slots with the scaling 1 -- the same maxima, bit for bit)
     for (int it = 0; it < passes; ++it) {
         A.iter = it;
         A.rmax = A.rmax_all + (int64_t)it * A.n;
+        const bool first = it == 0 && fused_pack;
         if (A.nf > 0) {
-            if (it == 0) hipLaunchKernelGGL((k_sweep_front<true, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
+            if (first) hipLaunchKernelGGL((k_sweep_front<true, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
             else hipLaunchKernelGGL((k_sweep_front<false, false>), dim3((unsigned)A.nf), dim3(64), sh, s, A);
         }
         if (A.n_big > 0) {
             const dim3 gb((unsigned)A.n_big, (unsigned)A.big_slices);
-            if (it == 0) hipLaunchKernelGGL((k_sweep_front<true, true>), gb, dim3(256), sh, s, A);
+            if (first) hipLaunchKernelGGL((k_sweep_front<true, true>), gb, dim3(256), sh, s, A);
             else hipLaunchKernelGGL((k_sweep_front<false, true>), gb, dim3(256), sh, s, A);
         }
         if (A.n_long > 0) {
@@ -4790,6 +4917,20 @@ hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool f
         if (forward) hipLaunchKernelGGL(k_solve_fwd_rg<3>, dim3(grid), dim3(64), kRgFwdLds, s, A, D);
         else hipLaunchKernelGGL(k_solve_bwd_rg<3>, dim3(grid), dim3(64), kRgBwdLds, s, A, D);
     }
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_bwd_flat(const SolveArgs& A, const DfArgs& D, int begin, int count, int lds_doubles, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    const size_t sh = (size_t)(lds_doubles + kSolveSlack) * sizeof(double) + 16;  // as the walk (launch_solve_df)
+    hipLaunchKernelGGL(k_solve_bwd_flat, dim3(count), dim3(64), sh, s, A, D, begin, count);
+    return hipGetLastError();
+}
+
+hipError_t launch_solve_fwd_flat(const SolveArgs& A, const DfArgs& D, int begin, int count, hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    // one wave per front; 6 waves per SIMD fit its registers
+    hipLaunchKernelGGL(k_solve_fwd_flat<6>, dim3(count), dim3(64), (192 + 8 * 33) * sizeof(double), s, A, D, begin, count);
     return hipGetLastError();
 }
 

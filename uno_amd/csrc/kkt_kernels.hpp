@@ -111,7 +111,10 @@ struct SolveArgs {
 
 // Dataflow (one launch per direction) solve schedule, kkt_kernels.hip k_solve_fwd_df / k_solve_bwd_df
 // walk-order front records of the dataflow solve: 16 int32 per position
-enum : int { kDescF = 0, kDescM, kDescP, kDescPar, kDescC0, kDescC1, kDescRo = 6, kDescLo = 8, kDescCvx = 10, kDescXs = 12 };
+// kDescNW: children whose arrival the front waits for (the forward walks' children; the flat levels solved by
+// k_solve_fwd_flat before the walk are not counted)
+enum : int { kDescF = 0, kDescM, kDescP, kDescPar, kDescC0, kDescC1, kDescRo = 6, kDescLo = 8, kDescCvx = 10, kDescXs = 12,
+             kDescNW = 14 };
 struct DfArgs {
     const int32_t* order;       // fronts, children before parents (the backward solve walks it from the end)
     const int32_t* desc;        // per walk position: 16-word record (kDesc* fields, 64-bit fields low word first)
@@ -135,6 +138,11 @@ struct DfArgs {
     int32_t rg_nf;
     const int32_t* ov_desc;     // ... the other fronts, same order, walked by the launch's last ov_grid blocks
     int32_t ov_nf, ov_grid;
+    const int32_t* rgf_desc;    // forward register walk: rg_desc without its flat levels (option solve_flat_levels)
+    int32_t rgf_nf;
+    const int32_t* flat_desc;   // the flat levels' fronts, level by level: one k_solve_fwd_flat launch per level
+    const int32_t* bdesc;       // the backward LDS-panel walk (k_solve_bwd_df): desc without the flat levels
+    int32_t bnf;
     unsigned long long* stamps; // diagnostics (nullptr in normal runs): per front and direction 4 s_memrealtime
                                 // words {start, dependency satisfied, values staged, published}
 };
@@ -203,7 +211,7 @@ struct SweepArgs {
     unsigned long long* counters = nullptr;  // reset by the first sweep's block 0 (k_reset_counters' values:
                                              // one launch less at the head of the factorization)
 };
-hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s);
+hipError_t launch_front_sweeps(const SweepArgs& A, int iters, hipStream_t s, bool fused_pack = true);
 hipError_t launch_pack_multi(const double* values, const int32_t* dup_ptr, const int32_t* dup_pos, const int32_t* multi,
                              int64_t count, double* uval, hipStream_t s);
 // ||A_pre||_inf from the scaling by original id (row scans over the packed slots, no row-major copy)
@@ -319,6 +327,10 @@ int solve_slack_doubles();
 int solve_rg_grid(bool forward, int nf, int waves_per_simd);  // waves_per_simd: 3 or 4 (the kernel variant)
 hipError_t launch_solve_bwd_w2(const SolveArgs& A, const int32_t* fronts, int count, hipStream_t s);
 hipError_t launch_solve_rg(const SolveArgs& A, const DfArgs& D, int grid, bool forward, int waves_per_simd, hipStream_t s);
+// the forward of the flat level's fronts DfArgs::flat_desc[begin, begin + count), one wave each, before the walk
+hipError_t launch_solve_fwd_flat(const SolveArgs& A, const DfArgs& D, int begin, int count, hipStream_t s);
+// the backward of the flat level's fronts, one wave each, after the backward walk (LDS: the walk's lds_doubles)
+hipError_t launch_solve_bwd_flat(const SolveArgs& A, const DfArgs& D, int begin, int count, int lds_doubles, hipStream_t s);
 hipError_t launch_solve_df(const SolveArgs& A, const DfArgs& D, int grid, int lds_doubles, bool forward, hipStream_t s);
 // rxpos for the dataflow backward solve (after every factorization); xpos: n int32 scratch.  Distributed
 // runs: the walk is the rank's own fronts, and the top rows (top_orig, eliminated on rank 0) get the

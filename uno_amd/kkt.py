@@ -253,13 +253,14 @@ class HipKKT:
 
     def debug_comm_trace(self, clear=False):
         """Transport calls recorded since the last clear (option comm_trace=1): list of (op, peer, bytes, redop),
-        op in send / recv / allreduce / broadcast / group_begin / group_end; None without a traced transport."""
+        op in send / recv / allreduce / broadcast / group_begin / group_end; before every send / recv / collective an
+        ("order", on_main_stream, unjoined_side_streams_mask, -1) record; None without a traced transport."""
         k = int(self.lib.uno_kkt_debug_comm_trace(self.h, None, 0, 0))
         if k < 0:
             return None
         buf = np.zeros(4 * max(k, 1), dtype=np.int64)
         self.lib.uno_kkt_debug_comm_trace(self.h, buf.ctypes.data_as(_i64p), len(buf), 1 if clear else 0)
-        names = ("send", "recv", "allreduce", "broadcast", "group_begin", "group_end")
+        names = ("send", "recv", "allreduce", "broadcast", "group_begin", "group_end", "order")
         return [(names[int(buf[4 * i])], int(buf[4 * i + 1]), int(buf[4 * i + 2]), int(buf[4 * i + 3])) for i in range(k)]
 
     def debug_scaling(self):
