@@ -1348,6 +1348,28 @@ __device__ __forceinline__ void reg_store(const S& st, int m, const double (&R)[
     }
 }
 
+// contribution block of a register-path front straight from the registers: element (i, j), p <= j <= i < m,
+// row-major packed lower triangle of order m - p (SC1: write-through stores for the dataflow hand-off)
+template <int G, int RM, bool SC1>
+__device__ __forceinline__ void write_cb_regs(const double (&R)[RM][RM], int m, int p, double* cb) {
+    if (m - p <= 0) return;
+    const int ty = threadIdx.x / G, tx = threadIdx.x % G;
+#pragma unroll
+    for (int a = 0; a < RM; ++a) {
+        const int i = ty + G * a;
+        if (G * (a + 1) <= p) continue;  // uniform: block entirely in the pivot rows
+#pragma unroll
+        for (int b = 0; b <= a; ++b) {
+            const int j = tx + G * b;
+            if (i < m && j >= p && j <= i) {
+                double* dst = cb + ((i - p) * (i - p + 1)) / 2 + (j - p);
+                if (SC1) st_sc1(dst, R[a][b]);
+                else *dst = R[a][b];
+            }
+        }
+    }
+}
+
 struct FrontShared {
     PivotDecision dec;
     int stuck;
@@ -1661,6 +1683,16 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             __syncthreads();
         }
     }
+    // dataflow kernel, one wave: the contribution block -- all the parent waits for -- is stored first, straight
+    // from the registers, and the parent signalled after ITS stores drain; L, the row maps and the counters follow
+    // (nothing in this launch reads them), so their stores no longer delay the hand-off up the tree
+    constexpr bool kEarlyCb = DF && REG && W == 1;
+    if constexpr (kEarlyCb) {
+        write_cb_regs<G, RM, true>(R, m, p, A.cb + A.cb_off[f]);
+        drain_stores();
+        if (tid == 0 && A.fparent[f] >= 0)
+            __hip_atomic_fetch_add(A.df_cnt + A.fparent[f], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if constexpr (REG && W == 1) {
         // L of the columns pivoted by the register path: column j (< p) still holds A(i, j) as it
         // was at step j, so L(i, j) = A(i, j) / d_j and L(j, j) = d_j, stored straight from the
@@ -1792,26 +1824,10 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     if (sub) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
     // ---- contribution block: row-major packed lower triangle of order cm = m - p ----
     const int cm = m - p;
-    if constexpr (REG && W == 1) {
-        // contribution block straight from the registers: element (i, j), p <= j <= i < m
-        if (cm > 0) {
-            double* cb = A.cb + A.cb_off[f];
-            const int ty = tid / G, tx = tid % G;
-#pragma unroll
-            for (int a = 0; a < RM; ++a) {
-                const int i = ty + G * a;
-                if (G * (a + 1) <= p) continue;  // uniform: block entirely in the pivot rows
-#pragma unroll
-                for (int b = 0; b <= a; ++b) {
-                    const int j = tx + G * b;
-                    if (i < m && j >= p && j <= i) {
-                        double* dst = cb + ((i - p) * (i - p + 1)) / 2 + (j - p);
-                        if (DF) st_sc1(dst, R[a][b]);
-                        else *dst = R[a][b];
-                    }
-                }
-            }
-        }
+    if constexpr (kEarlyCb) {
+        // stored above
+    } else if constexpr (REG && W == 1) {
+        write_cb_regs<G, RM, DF>(R, m, p, A.cb + A.cb_off[f]);
     } else if (cm > 0) {
         double* cb = A.cb + A.cb_off[f];
         const int ctot = cm * (cm + 1) / 2;
@@ -2097,11 +2113,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
     assemble_front<64, true>(st, fsize, m, p, lrow, sloc, rstage, A, f);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);  // signals the parent itself
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
-    const int par = A.fparent[f];
-    drain_stores();
-    if (par >= 0 && threadIdx.x == 0) __hip_atomic_fetch_add(A.df_cnt + par, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    static_assert(MR > 0, "k_factor_df runs the one-wave register path (factor_front signals the parent early)");
 }
 
 // ------------------------------------------------------------------------------------------------
