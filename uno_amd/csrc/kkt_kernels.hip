@@ -1370,6 +1370,14 @@ __device__ __forceinline__ void write_cb_regs(const double (&R)[RM][RM], int m, 
     }
 }
 
+// null-pivot threshold eps * null_fac * ||A_pre||_inf.  With anorm_bits == nullptr the norm is still being computed
+// on a second stream: the front is factored with threshold 0 and records the smallest pivot magnitude it accepted
+// (minpiv), which the host checks against the exact threshold.  The kernels load it at their start: read inside
+// factor_front (behind the assembly's barriers) it put one global round trip before every front's first pivot.
+__device__ __forceinline__ double front_thres(const FactorArgs& A) {
+    return A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
+}
+
 struct FrontShared {
     PivotDecision dec;
     int stuck;
@@ -1378,16 +1386,13 @@ struct FrontShared {
 
 // Factor one front (lower triangle in st), fully-summed columns 0..p-1.
 // Writes L (packed trapezoid), pivot kinds, permuted row ids, CB, inertia counters.
+// thres: the null-pivot threshold eps * null_fac * ||A_pre||_inf (front_thres), loaded by the caller at kernel start
 template <int NT, int MR, bool DF, class S>
 __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* lorig, int8_t* piv,
-                             double* coefA, double* coefB, const FactorArgs& A, int f, FrontShared* sh) {
+                             double* coefA, double* coefB, const FactorArgs& A, int f, FrontShared* sh, const double thres) {
     const int tid = threadIdx.x;
     for (int i = tid; i < m; i += NT) lorig[i] = i;  // local position before pivoting
     __syncthreads();
-    // null-pivot threshold eps * null_fac * ||A_pre||_inf; with anorm_bits == nullptr the norm is still
-    // being computed on a second stream: the front is factored with threshold 0 and records the
-    // smallest pivot magnitude it accepted (minpiv), which the host checks against the exact threshold
-    const double thres = A.anorm_bits ? DBL_EPSILON * A.null_fac * as_double(*A.anorm_bits) : 0.0;
     double minpiv = INFINITY;
     long long npos = 0, nneg = 0, nzero = 0, n2 = 0, nrel = 0, nstuck = 0;
     int nlds = 0;  // steps through the LDS path (search / interchanges / 2x2 / null)
@@ -1656,6 +1661,16 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         if constexpr (REG) reg_load<G, RM>(st, m, R);
         if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_reload += t - t8; t8 = t; }
     }
+    // dataflow kernel, one wave: the contribution block -- all the parent waits for -- is stored first, straight
+    // from the registers, and the parent signalled after ITS stores drain; L, the row maps and the counters follow
+    // (nothing in this launch reads them), so their stores (and the pivot bookkeeping below) no longer delay the hand-off up the tree
+    constexpr bool kEarlyCb = DF && REG && W == 1;
+    if constexpr (kEarlyCb) {
+        write_cb_regs<G, RM, true>(R, m, p, A.cb + A.cb_off[f]);
+        drain_stores();
+        if (tid == 0 && A.fparent[f] >= 0)
+            __hip_atomic_fetch_add(A.df_cnt + A.fparent[f], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     if constexpr (REG && W == 1) {
         // pivot kinds and inertia counts of the register path's 1x1 steps (recorded as bit masks in the loop)
         if ((fastpiv >> (tid & 63)) & 1) piv[tid & 63] = PIV_1X1;
@@ -1682,16 +1697,6 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             reg_store<G, RM>(st, m, R);
             __syncthreads();
         }
-    }
-    // dataflow kernel, one wave: the contribution block -- all the parent waits for -- is stored first, straight
-    // from the registers, and the parent signalled after ITS stores drain; L, the row maps and the counters follow
-    // (nothing in this launch reads them), so their stores no longer delay the hand-off up the tree
-    constexpr bool kEarlyCb = DF && REG && W == 1;
-    if constexpr (kEarlyCb) {
-        write_cb_regs<G, RM, true>(R, m, p, A.cb + A.cb_off[f]);
-        drain_stores();
-        if (tid == 0 && A.fparent[f] >= 0)
-            __hip_atomic_fetch_add(A.df_cnt + A.fparent[f], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if constexpr (REG && W == 1) {
         // L of the columns pivoted by the register path: column j (< p) still holds A(i, j) as it
@@ -2068,6 +2073,7 @@ template <int NT, int MR, int WPE = (MR > 8 ? 2 : 3)>
 __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_factor_lds(FactorArgs A, const int32_t* __restrict__ fronts) {
     extern __shared__ __attribute__((aligned(16))) double smem[];
     FrontShared* sh = reinterpret_cast<FrontShared*>(smem);  // first 32 B of the dynamic region
+    const double thres = front_thres(A);  // issued first: in flight during the assembly
     const int f = fronts[blockIdx.x];
     const int m = A.fm[f], p = A.fp[f];
     const PackedStore st{smem + 4};
@@ -2080,7 +2086,7 @@ __global__ __launch_bounds__(NT) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
     assemble_front<NT, false>(st, fsize, m, p, lrow, sloc, rstage, A, f);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front<NT, MR, false>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);
+    factor_front<NT, MR, false>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh, thres);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
 }
 
@@ -2102,6 +2108,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     const int t = (int)(tk - (A.df_epoch - 1u) * (uint32_t)A.df_nf);  // tickets are cumulative over launches
     if (t < 0 || t >= A.df_nf) return;  // cannot happen with one block per front
     const int f = A.df_order[t];
+    const double thres = front_thres(A);  // issued before the assembly: in flight under it
     const int m = A.fm[f], p = A.fp[f];
     const PackedStore st{smem + 4};
     const int64_t fsize = packed_even(m);
@@ -2113,7 +2120,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 0] = __builtin_amdgcn_s_memrealtime();
     assemble_front<64, true>(st, fsize, m, p, lrow, sloc, rstage, A, f);
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 1] = __builtin_amdgcn_s_memrealtime();
-    factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh);  // signals the parent itself
+    factor_front<64, MR, true>(st, m, p, lrow, rstage, pk, sloc, coefB, A, f, sh, thres);  // signals the parent itself
     if (A.stamps && threadIdx.x == 0) A.stamps[8 * f + 3] = __builtin_amdgcn_s_memrealtime();
     static_assert(MR > 0, "k_factor_df runs the one-wave register path (factor_front signals the parent early)");
 }
