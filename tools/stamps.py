@@ -64,6 +64,13 @@ if os.environ.get("MODE") == "8":  # LDS-path pivot steps by phase (a UKKT_STEP_
         print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | LDS steps/front {nl.mean():5.2f} | cycles per LDS step: "
               f"spill {per(4):6.0f} search {per(5):6.0f} swap+update {per(6):6.0f} reload {rel:6.0f} | loop {loop[s].mean():6.2f} us")
     sys.exit(0)
+if os.environ.get("MODE") == "9":  # a UKKT_STEP_STAMPS build: shader cycles (2.4 GHz, tools/clk) of the loop phase
+    for lev in range(fl.max() + 1):
+        s = fl == lev
+        c = st[s, 4:8].astype(np.float64) / 2400.0  # us
+        print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | reg_load {c[:,0].mean():6.2f} pivot loop {c[:,1].mean():6.2f} "
+              f"early CB+drain {c[:,2].mean():6.2f} bookkeeping+L {c[:,3].mean():6.2f} us | loop phase {loop[s].mean():6.2f} us")
+    sys.exit(0)
 if os.environ.get("MODE") == "3":
     w4, w5 = st[:, 4], st[:, 5]
     parts = np.stack([w4 & 0xffffffff, w4 >> 32, w5 & 0xffffffff, w5 >> 32, st[:, 6]], 1).astype(np.float64)

@@ -1409,6 +1409,15 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     constexpr bool st8 = false;
 #endif
     unsigned long long ls_spill = 0, ls_search = 0, ls_upd = 0, ls_reload = 0, t8 = 0;
+#ifdef UKKT_STEP_STAMPS
+    // MODE=9 (stamps build): shader cycles of reg_load, the pivot loop, the early contribution block + drain, and
+    // the bookkeeping + L write after it
+    const bool st9 = A.stamps != nullptr && A.stamp_mode == 9;
+#else
+    constexpr bool st9 = false;
+#endif
+    unsigned long long t9[5] = {0, 0, 0, 0, 0};
+    if (st9) t9[0] = __builtin_amdgcn_s_memtime();
     int k = 0;
     constexpr bool REG = MR > 0;
     constexpr int RM = MR > 0 ? MR : 1;
@@ -1434,6 +1443,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         if (W > 1 && tid == 0) sh->failk = -1;
         reg_load<G, RM>(st, m, R);
     }
+    if (st9) { __builtin_amdgcn_s_waitcnt(0); t9[1] = __builtin_amdgcn_s_memtime(); }
     while (k < p) {
         if constexpr (REG && W == 1) {
             // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of
@@ -1665,12 +1675,14 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // from the registers, and the parent signalled after ITS stores drain; L, the row maps and the counters follow
     // (nothing in this launch reads them), so their stores (and the pivot bookkeeping below) no longer delay the hand-off up the tree
     constexpr bool kEarlyCb = DF && REG && W == 1;
+    if (st9) t9[2] = __builtin_amdgcn_s_memtime();
     if constexpr (kEarlyCb) {
         write_cb_regs<G, RM, true>(R, m, p, A.cb + A.cb_off[f]);
         drain_stores();
         if (tid == 0 && A.fparent[f] >= 0)
             __hip_atomic_fetch_add(A.df_cnt + A.fparent[f], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+    if (st9) t9[3] = __builtin_amdgcn_s_memtime();
     if constexpr (REG && W == 1) {
         // pivot kinds and inertia counts of the register path's 1x1 steps (recorded as bit masks in the loop)
         if ((fastpiv >> (tid & 63)) & 1) piv[tid & 63] = PIV_1X1;
@@ -1723,9 +1735,12 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // columns still to be written from the LDS front (all when no register path ran)
     const bool lds_L = !(REG && W == 1) || fastmask != (p >= 64 ? ~0ull : ((1ull << p) - 1));
     const bool sub = A.stamps && A.stamp_mode == 2 && tid == 0;
+    if (st9) { __builtin_amdgcn_s_waitcnt(0); t9[4] = __builtin_amdgcn_s_memtime(); }
     if (A.stamps && tid == 0) {
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
-        if (st8) {
+        if (st9) {
+            for (int q = 0; q < 4; ++q) A.stamps[8 * f + 4 + q] = t9[q + 1] - t9[q];
+        } else if (st8) {
             A.stamps[8 * f + 4] = ls_spill;
             A.stamps[8 * f + 5] = ls_search;
             A.stamps[8 * f + 6] = ls_upd;
