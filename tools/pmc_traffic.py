@@ -9,7 +9,7 @@ import json
 import sys
 
 fe, wr, out = (json.load(open(sys.argv[1])), json.load(open(sys.argv[2])), sys.argv[3])
-script = sys.argv[4] if len(sys.argv) > 4 else "tools/profile_r04.sh"
+script = sys.argv[4] if len(sys.argv) > 4 else "tools/profile_r06.sh"
 pf, pw = fe["per_run"], wr["per_run"]
 kb = 1024.0
 res = {
