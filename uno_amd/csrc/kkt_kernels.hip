@@ -1402,7 +1402,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // per-step cycle counters only in a build with UKKT_STEP_STAMPS (a runtime flag costs VALU / SALU in every
     // pivot step); the phase stamps (assembly / loop / write-out) need no flag here
 #ifdef UKKT_STEP_STAMPS
-    const bool stamping = A.stamps != nullptr && A.stamp_mode != 7;
+    const bool stamping = A.stamps != nullptr && A.stamp_mode != 7 && A.stamp_mode != 9;  // MODE 9: phases only
     const bool st8 = A.stamps != nullptr && A.stamp_mode == 8;  // LDS-path steps by phase (stamps.py MODE=8)
 #else
     constexpr bool stamping = false;
