@@ -1492,9 +1492,14 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                     // LDS round trip
                     double dinv = 1.0 / akk;
                     asm volatile("" : "+v"(dinv));
-                    bool bad = (tid > k) & (tid < NR) & (A.u * fabs(t0) > aak);
-                    if constexpr (NR > 64) bad = bad | ((tid < NR - 64) & (tid + 64 > k) & (A.u * fabs(t1) > aak));
-                    need = (__ballot(bad) != 0) || !(aak > thres);
+                    // the candidate's product, 0 for rows that are not candidates (0 > aak never holds): one DP compare
+                    // feeds the ballot directly
+                    double tv = ((tid > k) & (tid < NR)) ? A.u * fabs(t0) : 0.0;
+                    if constexpr (NR > 64) {
+                        const double tv1 = ((tid < NR - 64) & (tid + 64 > k)) ? A.u * fabs(t1) : 0.0;
+                        tv = fmax(tv, tv1);  // max: "either exceeds aak" (tv1 is never NaN-vs-number ambiguous: |x| * u)
+                    }
+                    need = (__ballot(tv > aak) != 0) || !(aak > thres);
                     if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_search += t - t_mark; t_mark = t; }
                     if (!need) {  // 1x1 pivot at k without interchange (k < 64: its |a_kk| enters minpiv after the loop)
                         double cv[RM];
@@ -1507,7 +1512,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
                             for (int b = bk; b <= a; ++b) R[a][b] -= lv[a] * cv[b];
                         if (k < 64) {  // uniform
                             fastpiv |= 1ull << k;
-                            fastneg |= (akk > 0.0 ? 0ull : 1ull) << k;
+                            // an accepted pivot is nonzero (|a_kk| > thres >= 0), so "not positive" is its sign bit: a
+                            // scalar shift of the uniform akk (no VALU compare -> readfirstlane -> SALU hop in the step)
+                            fastneg |= (as_bits(akk) >> 63) << k;
                         } else {  // columns beyond the masks (fronts of 65..72 columns after delays): per step
                             minpiv = fmin(minpiv, aak);
                             if (tid == 0) { piv[k] = PIV_1X1; if (akk > 0.0) npos++; else nneg++; }
@@ -4787,6 +4794,7 @@ __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restr
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
                         unsigned long long* counters, unsigned long long* minbits, hipStream_t s, const uint32_t* abort_word,
                         unsigned long long* host_out) {
+    // (1024 blocks, one front per thread, measured no faster than 64: more same-address atomics; round 6)
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(64, (nf + 255) / 256));
     if (nf <= 0 && host_out == nullptr) return hipSuccess;
     hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, fmin, nf, counters, minbits, abort_word, host_out);
@@ -4998,6 +5006,7 @@ hipError_t launch_xs_out(const double* xs, const double* scale, const int32_t* x
 hipError_t launch_xpos(const SolveArgs& A, const DfArgs& D, int32_t* xpos, int32_t* rxpos, const int32_t* top_orig,
                        int64_t n_top, int64_t top_base, hipStream_t s, bool pass0) {
     if (D.nf <= 0) return hipSuccess;
+    // (one row per thread instead of the 4096-block cap measured no faster: round 6)
     const dim3 g(grid_for(D.rows_total, 256));
     if (pass0) hipLaunchKernelGGL(k_xpos, g, dim3(256), 0, s, D, A.frow, xpos, rxpos, 0);
     if (n_top > 0) hipLaunchKernelGGL(k_xpos_top, dim3(grid_for(n_top, 256)), dim3(256), 0, s, top_orig, n_top, top_base, xpos);
