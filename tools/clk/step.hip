@@ -113,7 +113,7 @@ void steps(unsigned long long* o, double* s) {
 }
 int main() {
     unsigned long long* o; double* s;
-    (void)hipMalloc(&o, 64); (void)hipMalloc(&s, 64 * 8);
+    (void)hipMalloc(&o, 256); (void)hipMalloc(&s, 64 * 8);
     run<true, true, true, true>("full step", o, s);
     run<false, true, true, true>("no division", o, s);
     run<true, false, true, true>("no LDS publish/read", o, s);

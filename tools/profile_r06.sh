@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round-6 evidence of the final tree (C3 unless noted), into gpurun_out/r05f: bench line (CPU baseline +
+# Round-6 evidence of the final tree (C3 unless noted), into gpurun_out/r06/final: bench line (CPU baseline +
 # shipped-mode line), rocprofv3 kernel-trace stats, one-step timeline, FETCH_SIZE / WRITE_SIZE passes
 # (steady-state factorizations -> pmc_traffic.json), two SQ counter passes, the same-size N=1 point of the
 # distributed curve and the IPM-sequence leg.  Large fronts: tools/bigfront_bench.py.

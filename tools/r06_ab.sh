@@ -1,5 +1,5 @@
 # A/B of the in-tree library (B) against $A_LIB (A) on the C3 bench line, alternated twice, after the parity files
-# given in $TESTS (default: the GPU parity suite + null threshold):  OUT=name A_LIB=ab/x/libuno_kkt.so bash tools/r06_ab.sh
+# given in $TESTS (B_LIB: another library as B) (default: the GPU parity suite + null threshold):  OUT=name A_LIB=ab/x/libuno_kkt.so bash tools/r06_ab.sh
 set -e
 export TMPDIR=/tmp
 R=gpurun_out/r06/${OUT:-ab}
@@ -11,7 +11,7 @@ if [ "$TESTS" != "none" ]; then
 fi
 for i in 1 2; do
   UNO_KKT_LIB=${A_LIB} timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS} ${A_ARGS} > $R/a$i.json 2> $R/a$i.err
-  timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS} ${B_ARGS} > $R/b$i.json 2> $R/b$i.err
+  UNO_KKT_LIB=${B_LIB} timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline ${BENCH_ARGS} ${B_ARGS} > $R/b$i.json 2> $R/b$i.err
 done
 OUT=${OUT:-ab} python - <<'PY'
 import json, os

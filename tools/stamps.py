@@ -71,6 +71,30 @@ if os.environ.get("MODE") == "9":  # a UKKT_STEP_STAMPS build: shader cycles (2.
         print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | reg_load {c[:,0].mean():6.2f} pivot loop {c[:,1].mean():6.2f} "
               f"early CB+drain {c[:,2].mean():6.2f} bookkeeping+L {c[:,3].mean():6.2f} us | loop phase {loop[s].mean():6.2f} us")
     sys.exit(0)
+if os.environ.get("MODE") == "11":  # dataflow hand-off: child signalled -> parent sees it -> children assembled
+    par = np.full(nf, -1, dtype=np.int64)
+    lib.uno_kkt_debug_front_parent = getattr(lib, "uno_kkt_debug_front_parent", None)
+    # parents from the level structure: a front's parent is the unique front of the next level whose rows...
+    # (not exported) -- use the timeline instead: per level, the latest child signal vs the level's arrivals
+    for lev in range(1, fl.max() + 1):
+        s = fl == lev
+        c = fl == lev - 1
+        seen = st[s, 4]; sig_prev = st[c, 5]; done_asm = st[s, 6]
+        if (seen == 0).all() or (sig_prev == 0).all():
+            continue
+        print(f"level {lev:2d} fronts {s.sum():5d} | children assembled - arrival seen {((done_asm - seen) * 10e-3).mean():6.2f} us | "
+              f"arrival seen - last signal of level {lev - 1} {((seen.max() - sig_prev[sig_prev > 0].max()) * 10e-3):7.2f} us (max - max) | "
+              f"loop start - children assembled {((st[s, 1] - done_asm) * 10e-3).mean():5.2f} us")
+    sys.exit(0)
+if os.environ.get("MODE") == "10":  # any build: real-time phase boundaries inside the loop phase
+    for lev in range(fl.max() + 1):
+        s = fl == lev
+        rl = (st[s, 4] - st[s, 1]) * 10e-3; pv = (st[s, 5] - st[s, 4]) * 10e-3
+        cb = (st[s, 6] - st[s, 5]) * 10e-3; rest = (st[s, 2] - st[s, 6]) * 10e-3
+        print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | reg_load {rl.mean():6.2f} pivot loop {pv.mean():6.2f} "
+              f"({pv.mean() * 1e3 / max(fp[s].mean(), 1):5.0f} ns/step) early CB+drain {cb.mean():6.2f} bookkeeping+L {rest.mean():6.2f} us | "
+              f"loop phase {loop[s].mean():6.2f} us")
+    sys.exit(0)
 if os.environ.get("MODE") == "3":
     w4, w5 = st[:, 4], st[:, 5]
     parts = np.stack([w4 & 0xffffffff, w4 >> 32, w5 & 0xffffffff, w5 >> 32, st[:, 6]], 1).astype(np.float64)

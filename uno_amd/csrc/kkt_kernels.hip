@@ -1418,6 +1418,9 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
 #endif
     unsigned long long t9[5] = {0, 0, 0, 0, 0};
     if (st9) t9[0] = __builtin_amdgcn_s_memtime();
+    // MODE 10 (any build): the same phase boundaries on the 100 MHz real-time clock, no per-step code
+    const bool st10 = A.stamps != nullptr && A.stamp_mode == 10;
+    unsigned long long r10[4] = {0, 0, 0, 0};
     int k = 0;
     constexpr bool REG = MR > 0;
     constexpr int RM = MR > 0 ? MR : 1;
@@ -1444,6 +1447,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         reg_load<G, RM>(st, m, R);
     }
     if (st9) { __builtin_amdgcn_s_waitcnt(0); t9[1] = __builtin_amdgcn_s_memtime(); }
+    if (st10) { __builtin_amdgcn_s_waitcnt(0); r10[0] = __builtin_amdgcn_s_memrealtime(); }
     while (k < p) {
         if constexpr (REG && W == 1) {
             // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of
@@ -1683,13 +1687,16 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     // (nothing in this launch reads them), so their stores (and the pivot bookkeeping below) no longer delay the hand-off up the tree
     constexpr bool kEarlyCb = DF && REG && W == 1;
     if (st9) t9[2] = __builtin_amdgcn_s_memtime();
+    if (st10) r10[1] = __builtin_amdgcn_s_memrealtime();
     if constexpr (kEarlyCb) {
         write_cb_regs<G, RM, true>(R, m, p, A.cb + A.cb_off[f]);
         drain_stores();
         if (tid == 0 && A.fparent[f] >= 0)
             __hip_atomic_fetch_add(A.df_cnt + A.fparent[f], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (A.stamps && A.stamp_mode == 11 && tid == 0) A.stamps[8 * f + 5] = __builtin_amdgcn_s_memrealtime();  // signalled
     }
     if (st9) t9[3] = __builtin_amdgcn_s_memtime();
+    if (st10) r10[2] = __builtin_amdgcn_s_memrealtime();
     if constexpr (REG && W == 1) {
         // pivot kinds and inertia counts of the register path's 1x1 steps (recorded as bit masks in the loop)
         if ((fastpiv >> (tid & 63)) & 1) piv[tid & 63] = PIV_1X1;
@@ -1747,6 +1754,13 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         A.stamps[8 * f + 2] = __builtin_amdgcn_s_memrealtime();
         if (st9) {
             for (int q = 0; q < 4; ++q) A.stamps[8 * f + 4 + q] = t9[q + 1] - t9[q];
+        } else if (A.stamp_mode == 11) {
+            // [4], [5], [6] written above
+        } else if (st10) {
+            A.stamps[8 * f + 4] = r10[0];
+            A.stamps[8 * f + 5] = r10[1];
+            A.stamps[8 * f + 6] = r10[2];
+            A.stamps[8 * f + 7] = (unsigned long long)p;
         } else if (st8) {
             A.stamps[8 * f + 4] = ls_spill;
             A.stamps[8 * f + 5] = ls_search;
@@ -2007,6 +2021,8 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
     if (asm_st) { __builtin_amdgcn_s_waitcnt(0); A.stamps[8 * f + 5] = __builtin_amdgcn_s_memrealtime(); }
     // dataflow schedule: children factored in this launch have published their contribution blocks
     if (DF && A.df_nch[f] > 0) df_wait(A.df_cnt + f, A.df_epoch * (uint32_t)A.df_nch[f], A.df_abort);
+    // MODE 11 (dataflow hand-off): [4] the children's arrival seen, [6] the children assembled (below)
+    if (DF && A.stamps && A.stamp_mode == 11 && tid == 0) A.stamps[8 * f + 4] = __builtin_amdgcn_s_memrealtime();
     // children: contribution blocks are row-major packed lower triangles (row r: columns 0..r);
     // relmap maps child CB rows to ascending parent rows, so (rm[r], rm[c]) is in the lower triangle.
     // Children are taken in pairs whose first batches are loaded together (the loads of a child are
@@ -2017,14 +2033,18 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
         double v[CB];
         int pos[CB];
     };
-    auto load_batch = [&](const double* cb, const int32_t* rm, const uint16_t* cp, int ctot, int t0, Batch& b) {
-        if (cp) {  // the entries' positions in this front, precomputed (FactorArgs::cbpos): no relmap gathers
+    // the entries' positions in this front, precomputed (FactorArgs::cbpos): no relmap gathers
+    auto load_batch_pos = [&](const double* cb, const uint16_t* cp, int ctot, int t0, Batch& b) {
 #pragma unroll
-            for (int u = 0; u < CB; ++u) {
-                const int t = t0 + u * NT;
-                b.v[u] = t < ctot ? (DF ? ld_sc1(cb + t) : cb[t]) : 0.0;
-                b.pos[u] = t < ctot ? (int)cp[t] : -1;
-            }
+        for (int u = 0; u < CB; ++u) {
+            const int t = t0 + u * NT;
+            b.v[u] = t < ctot ? (DF ? ld_sc1(cb + t) : cb[t]) : 0.0;
+            b.pos[u] = t < ctot ? (int)cp[t] : -1;
+        }
+    };
+    auto load_batch = [&](const double* cb, const int32_t* rm, const uint16_t* cp, int ctot, int t0, Batch& b) {
+        if (cp) {
+            load_batch_pos(cb, cp, ctot, t0, b);
             return;
         }
         int32_t gi[CB], gj[CB];
@@ -2065,19 +2085,34 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
             const uint16_t* cpa = A.cbpos ? A.cbpos + (int64_t)readlane64(my_cbo, q) : nullptr;
             const uint16_t* cpb = A.cbpos && two ? A.cbpos + (int64_t)readlane64(my_cbo, q + 1) : nullptr;
             const int ta = cma > 0 ? cma * (cma + 1) / 2 : 0, tb = cmb > 0 ? cmb * (cmb + 1) / 2 : 0;
-            Batch ba, bb;
+            Batch ba, bb, ba2;
             load_batch(cba, rma, cpa, ta, tid, ba);
             load_batch(cbb, rmb, cpb, tb, tid, bb);
+            // the second batch of child a in flight with the first batches, and child b's second batch issued before
+            // b's first is added (into a's registers, free by then): contribution blocks of up to 2 NT CB entries (63
+            // rows at one wave: every one-wave front's children) no longer cost three round trips in sequence (round
+            // 6: 3.0 - 3.8 us of children assembly per level of the upper-tree chain).  Three batches live at most:
+            // a fourth spills the 168-VGPR kernels.
+            // (the precomputed-position path only: the relmap path's loop-invariant row/column decodes of a second
+            // batch, hoisted out of the children loop by the compiler, would spill)
+            // (the dataflow kernel only, where the hand-off chain waits on it: the level kernels keep 4 waves per SIMD
+            // at MR = 4 without the third batch)
+            const bool a2 = DF && cpa && ta > NT * CB, b2 = DF && cpb && tb > NT * CB;  // uniform
+            if (a2) load_batch_pos(cba, cpa, ta, NT * CB + tid, ba2);
             add_batch(ba);
-            // rest of a / b (CBs of more than 45 rows at one wave): uniform loops, so the barrier
-            // below is reached by every wave
-            for (int base = NT * CB; base < ta; base += NT * CB) {
+            if (a2) add_batch(ba2);
+            // rest of a / b: uniform loops, so the barrier below is reached by every wave; the additions stay child by
+            // child, batch by batch (the same order as before)
+            for (int base = (a2 ? 2 : 1) * NT * CB; base < ta; base += NT * CB) {
                 load_batch(cba, rma, cpa, ta, base + tid, ba);
                 add_batch(ba);
             }
+            __builtin_amdgcn_sched_barrier(0);  // keep b's second batch after a's additions (a fourth live batch spills)
+            if (b2) load_batch_pos(cbb, cpb, tb, NT * CB + tid, ba);
             if (NT > 64) __syncthreads();  // children may overlap: one child at a time
             add_batch(bb);
-            for (int base = NT * CB; base < tb; base += NT * CB) {
+            if (b2) add_batch(ba);
+            for (int base = (b2 ? 2 : 1) * NT * CB; base < tb; base += NT * CB) {
                 load_batch(cbb, rmb, cpb, tb, base + tid, bb);
                 add_batch(bb);
             }
@@ -2085,7 +2120,7 @@ __device__ void assemble_front_pre(const S& st, int64_t fsize, const FrontMeta& 
         }
     }
     __syncthreads();
-    if (asm_st) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
+    if (asm_st || (DF && A.stamps && A.stamp_mode == 11 && tid == 0)) A.stamps[8 * f + 6] = __builtin_amdgcn_s_memrealtime();
 }
 
 // LDS layout of one front: [FrontShared 32 B][packed lower m(m+1)/2, even][sloc m][coefB m]
