@@ -63,6 +63,13 @@ if os.environ.get("MODE") == "8":  # LDS-path pivot steps by phase (a UKKT_STEP_
         rel = ((st[s, 7] & 0xffffffffff).sum() / max(tot, 1))
         print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | LDS steps/front {nl.mean():5.2f} | cycles per LDS step: "
               f"spill {per(4):6.0f} search {per(5):6.0f} swap+update {per(6):6.0f} reload {rel:6.0f} | loop {loop[s].mean():6.2f} us")
+    if os.environ.get("TAILS"):  # the slowest loops per level: LDS steps and their cycles (totals per front)
+        for lev in range(fl.max() + 1):
+            s = np.nonzero(fl == lev)[0]
+            o = s[np.argsort(-loop[s])[:3]]
+            print(f"level {lev:2d} slowest loops: " + ", ".join(
+                f"f{f} m{fm[f]} p{fp[f]} loop {loop[f]:.1f} us LDS steps {n_l[f]} spill {st[f,4]} search {st[f,5]} "
+                f"upd {st[f,6]} reload {st[f,7] & 0xffffffffff}" for f in o))
     sys.exit(0)
 if os.environ.get("MODE") == "9":  # a UKKT_STEP_STAMPS build: shader cycles (2.4 GHz, tools/clk) of the loop phase
     for lev in range(fl.max() + 1):
@@ -103,6 +110,16 @@ if os.environ.get("MODE") == "3":
         per = parts[s] / steps[s][:, None]
         print(f"level {lev:2d} m {fm[s].mean():5.1f} p {fp[s].mean():5.1f} | per step: akk {per[:,0].mean():6.0f} test {per[:,1].mean():6.0f} "
               f"ballot {per[:,2].mean():6.0f} reads {per[:,3].mean():6.0f} fma {per[:,4].mean():6.0f} | loop {loop[s].mean():6.2f} us")
+    sys.exit(0)
+if os.environ.get("ENDS"):  # per level: end-time percentiles and the latest-ending fronts (start / assembled / end)
+    t0 = st[:, 0].min()
+    for lev in range(fl.max() + 1):
+        s = np.nonzero(fl == lev)[0]
+        e = (st[s, 3] - t0) * 10e-3
+        q = np.percentile(e, [50, 90, 99, 100])
+        o = s[np.argsort(-e)[:4]]
+        print(f"level {lev:2d} end p50 {q[0]:7.1f} p90 {q[1]:7.1f} p99 {q[2]:7.1f} max {q[3]:7.1f} | latest: " + ", ".join(
+            f"f{f} m{fm[f]} p{fp[f]} [{(st[f,0]-t0)*10e-3:.1f} {(st[f,1]-t0)*10e-3:.1f} {(st[f,3]-t0)*10e-3:.1f}]" for f in o))
     sys.exit(0)
 if os.environ.get("TAILS"):  # per level: the slowest fronts (the level's tail) -- loop / write maxima and who
     for lev in range(fl.max() + 1):

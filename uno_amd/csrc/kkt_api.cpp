@@ -11,6 +11,7 @@
 #include <cmath>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -534,7 +535,21 @@ hipError_t build_plan(uno_kkt_t h, Pred take, Plan& P) {
         // front).  Finer LDS classes ({16, 24, .., 128}) were measured slower on C3 (2.36 vs 1.99 ms):
         // the one-wave kernel is VALU-issue bound at levels 0-1 and more co-resident fronts per CU
         // only lengthen every front; a class smaller than kMinClass absorbs the next smaller one.
-        static const std::vector<int> caps{32, 64, kMaxWaveFront, 128};  // LDS size classes
+        static const std::vector<int> caps = [] {  // LDS size classes; UNO_KKT_CAPS: experiments
+            std::vector<int> c{32, 64, kMaxWaveFront, 128};
+            if (const char* e = getenv("UNO_KKT_CAPS")) {
+                std::vector<int> v;
+                for (const char* q = e; *q;) {
+                    char* end = nullptr;
+                    const long x = strtol(q, &end, 10);
+                    if (end == q) break;
+                    v.push_back((int)x);
+                    q = *end ? end + 1 : end;
+                }
+                if (!v.empty()) c = v;
+            }
+            return c;
+        }();
         constexpr int kMinClass = 2048;
         auto prev_cap = [](int c) {
             int pc = 0;

@@ -1657,9 +1657,13 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             const double dk = st.at(k, k);
             const double dinv = 1.0 / dk;
             if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_rest += t - t_mark; t_mark = t; }
-            // rare fallback steps of the register path use the low-register generic update, so the
-            // kernel's VGPR budget (occupancy) is set by the register-resident fast path
-            schur_update_generic<kGrid<NT>, false>(st, m, k, dinv, 0.0, 0.0);
+            // register path: the register front is dead here (reloaded after the step), so the tiled update (reads
+            // batched per row block, no per-element LDS round trip) fits the fast path's VGPR budget; round 6:
+            // ~9 000 shader cycles per LDS step in the generic loop, and the dataflow chain's slowest fronts are
+            // the ones with ~10 such steps (delayed columns).  Same products and order: bit-identical.  (MR = 9:
+            // the tile's 9 row blocks spill the 2-wave budget; generic there)
+            if constexpr (REG && RM <= 8) schur_update_tile<G, RM, false>(st, m, k, dinv, 0.0, 0.0);
+            else schur_update_generic<kGrid<NT>, false>(st, m, k, dinv, 0.0, 0.0);
             if (tid == 0) { piv[k] = PIV_1X1; if (dk > 0.0) npos++; else nneg++; }
             __syncthreads();
             if (stamping) { unsigned long long t = __builtin_amdgcn_s_memtime(); cyc_update += t - t_mark; t_mark = t; }
@@ -1668,7 +1672,8 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             const double a = st.at(k, k), b = st.at(k + 1, k), e = st.at(k + 1, k + 1);
             const double det = a * e - b * b;
             const double idet = 1.0 / det;
-            schur_update_generic<kGrid<NT>, true>(st, m, k, a * idet, b * idet, e * idet);
+            if constexpr (REG && RM <= 8) schur_update_tile<G, RM, true>(st, m, k, a * idet, b * idet, e * idet);
+            else schur_update_generic<kGrid<NT>, true>(st, m, k, a * idet, b * idet, e * idet);
             if (tid == 0) {
                 piv[k] = PIV_2X2_A; piv[k + 1] = PIV_2X2_B; n2++;
                 if (det < 0.0) { npos++; nneg++; }
