@@ -1448,8 +1448,13 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
     }
     if (st9) { __builtin_amdgcn_s_waitcnt(0); t9[1] = __builtin_amdgcn_s_memtime(); }
     if (st10) { __builtin_amdgcn_s_waitcnt(0); r10[0] = __builtin_amdgcn_s_memrealtime(); }
+    // one-wave register path: the front is current in LDS only -- the step after an LDS step failed the same test
+    // (quick_1x1 on the LDS front, the register path's test restated), so it runs in LDS without the reload and the
+    // spill between (~3 300 shader cycles per step on the delayed-column fronts, whose LDS steps come in runs)
+    bool in_lds = false;
     while (k < p) {
         if constexpr (REG && W == 1) {
+          if (!in_lds) {
             // One wave owns the whole front (m <= G * RM): column k lives in register R[.][k / G] of
             // the lanes with tx = k % G.  Those lanes test it in place (one compare per row block,
             // one ballot) and publish it to an LDS vector (one store per block) that every lane reads
@@ -1535,6 +1540,7 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             reg_store<G, RM>(st, m, R);
             __syncthreads();
             if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_spill += t - t8; t8 = t; }
+          }
         } else if constexpr (REG) {
             const int ty = tid / G, tx = tid % G;
             bool need = false;
@@ -1684,7 +1690,20 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
             k += 2;
         }
         if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_upd += t - t8; t8 = t; }
-        if constexpr (REG) reg_load<G, RM>(st, m, R);
+        if constexpr (REG && W == 1) {
+            in_lds = k < p && !quick_1x1(st, m, k, A.u, thres);  // uniform (ballot)
+            if (!in_lds) {
+                reg_load<G, RM>(st, m, R);
+            } else {
+                // the registers are stale until the reload: tell the compiler (no value to keep across the LDS steps)
+#pragma unroll
+                for (int a = 0; a < RM; ++a)
+#pragma unroll
+                    for (int b = 0; b < RM; ++b) R[a][b] = __builtin_nondeterministic_value(R[a][b]);
+            }
+        } else if constexpr (REG) {
+            reg_load<G, RM>(st, m, R);
+        }
         if (st8) { const unsigned long long t = __builtin_amdgcn_s_memtime(); ls_reload += t - t8; t8 = t; }
     }
     // dataflow kernel, one wave: the contribution block -- all the parent waits for -- is stored first, straight
