@@ -4,6 +4,8 @@ set -e
 export TMPDIR=/tmp
 R=gpurun_out/r06/${OUT:-ab}
 mkdir -p $R
+( while true; do date >> $R/heartbeat.log; sleep 30; done ) &  # long tests print nothing for minutes
+HB=$!; trap "kill $HB" EXIT
 TESTS=${TESTS:-tests/test_gpu_parity.py tests/test_null_threshold.py}
 if [ "$TESTS" != "none" ]; then
   timeout -k 10 600 python -u -m pytest -x -q -m gpu --timeout 300 --timeout-method thread $TESTS > $R/t.log 2>&1

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 #include <chrono>
@@ -237,6 +238,9 @@ struct uno_kkt {
     hipEvent_t ev_counters = nullptr;  // after the counters' read-back of the last enqueued factorization
     hipEvent_t ev_wait = nullptr;      // host_wait_stream
     int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
+    int host_flag = 1;                 // option "host_flag": one GPU, the factorization's counters by k_count's flag
+    unsigned long long count_seq = 0;  // k_count flags issued
+    unsigned long long wait_seq = 0;   // the flag the last enqueued factorization writes (0: wait on ev_counters)
     DBuf<unsigned long long> rmaxk;    // front sweeps: n row maxima per sweep (elimination order)
     DBuf<int32_t> rows_sw;             // front sweeps: the fronts' rows in the elimination order
     DBuf<int8_t> longpos_sw;           // front sweeps: longpos by new index
@@ -841,8 +845,30 @@ hipError_t host_wait_stream(uno_kkt_t h, hipStream_t s) {
     return e != hipSuccess ? e : host_wait(h, h->ev_wait);
 }
 
+// Host wait for k_count's sequence number in the page-locked block (slot 10, written after the counters with
+// system-scope stores): a device error or a stream that finished without it ends the wait
+hipError_t host_wait_flag(uno_kkt_t h, unsigned long long seq) {
+    volatile unsigned long long* flag = h->h_counters + 10;
+    for (unsigned it = 1;; ++it) {
+        if (*flag == seq) break;
+        if ((it & 255) == 0) {
+            const hipError_t e = hipStreamQuery(h->stream);
+            if (e == hipSuccess) {
+                if (*flag == seq) break;
+                return hipErrorUnknown;  // the stream is done and the flag never came
+            }
+            if (e != hipErrorNotReady) return e;
+        }
+        __builtin_ia32_pause();
+    }
+    std::atomic_thread_fence(std::memory_order_acquire);
+    return hipSuccess;
+}
+
 int sync_and_verify(uno_kkt_t h) {
-    HIPCHK(h, host_wait(h, h->ev_counters));  // the counters (and the dataflow abort word) are on the host
+    // the counters (and the dataflow abort word) are on the host
+    if (h->wait_seq) HIPCHK(h, host_wait_flag(h, h->wait_seq));
+    else HIPCHK(h, host_wait(h, h->ev_counters));
     uint32_t ab = 0;
     memcpy(&ab, h->h_counters + 11, sizeof(ab));
     if (ab != 0) {
@@ -1684,9 +1710,12 @@ int enqueue_factorization(uno_kkt_t h) {
             }
         }
     }
+    h->wait_seq = 0;
     if (h->world == 1) {  // counters and the dataflow abort word straight into the page-locked host block
+        // option host_flag (with spin_wait): the host polls the sequence number k_count writes last
+        if (h->host_flag && h->spin_wait) h->wait_seq = ++h->count_seq;
         HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits_p, s,
-                               dff ? h->df_abort.p : nullptr, h->h_counters));
+                               dff ? h->df_abort.p : nullptr, h->h_counters, h->wait_seq));
     } else {
         HIPCHK(h, launch_count(h->fcnt.p, h->fstat.p, h->fmin.p, S.nf, h->counters.p, h->minbits_p, s));
     }
@@ -1697,7 +1726,9 @@ int enqueue_factorization(uno_kkt_t h) {
     }
     // counters and minbits in one copy (h_counters[8] is the min pivot bits)
     if (h->world > 1) HIPCHK(h, hipMemcpyAsync(h->h_counters, h->counters.p, 9 * sizeof(unsigned long long), hipMemcpyDeviceToHost, s));
-    HIPCHK(h, hipEventRecord(h->ev_counters, s));  // sync_and_verify waits for this, not for the xpos below
+    // sync_and_verify waits for this, not for the xpos below (or for k_count's flag: no event marker between
+    // k_count and the xpos launch)
+    if (!h->wait_seq) HIPCHK(h, hipEventRecord(h->ev_counters, s));
     h->factor_enqueued = true;
     h->df_rx_valid = false;  // pivoting may have permuted rows
     HIPCHK(h, enqueue_xpos(h));
@@ -1813,6 +1844,7 @@ int uno_kkt_set_option(uno_kkt_t h, const char* name, double value) {
     else if (n == "concurrent_classes") h->concurrent_classes = (int)value;
     else if (n == "early_xpos") h->early_xpos = value != 0.0;
     else if (n == "spin_wait") h->spin_wait = value != 0.0;
+    else if (n == "host_flag") h->host_flag = value != 0.0;
     else if (n == "front_scale") h->front_scale = std::max(0, std::min(2, (int)value));
     else if (n == "debug_abort_solves") h->debug_abort_solves = std::max(0, (int)value);
     else if (n == "dist_min_efficiency") h->dist_min_eff = value;

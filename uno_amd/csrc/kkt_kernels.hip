@@ -4803,7 +4803,7 @@ __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restr
                                                const int32_t* __restrict__ fstat, const double* __restrict__ fmin,
                                                int64_t nf, unsigned long long* __restrict__ counters,
                                                unsigned long long* __restrict__ minbits, const uint32_t* __restrict__ abort_word,
-                                               unsigned long long* __restrict__ host_out) {
+                                               unsigned long long* __restrict__ host_out, unsigned long long seq) {
     unsigned long long acc[6] = {0, 0, 0, 0, 0, 0};
     unsigned long long mn = ~0ull;
     // four fronts per thread and trip, their loads issued together (one memory round trip per four fronts, not
@@ -4858,18 +4858,27 @@ __global__ void __launch_bounds__(256) k_count(const unsigned long long* __restr
     __syncthreads();
     if (!last) return;
     __threadfence();
+    // system-scope (write-through) stores, drained, then the sequence number in slot 10 that the host polls
+    // (option host_flag): the host sees the counters without waiting for the kernel's end and its completion
+    // signal (no event marker in the stream; no system-scope release either, which would write back the L2)
     if (threadIdx.x < 9)
-        host_out[threadIdx.x] = __hip_atomic_load(counters + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (threadIdx.x == 11) host_out[11] = abort_word ? (unsigned long long)__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull;
+        __hip_atomic_store(host_out + threadIdx.x, __hip_atomic_load(counters + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x == 11)
+        __hip_atomic_store(host_out + 11, abort_word ? (unsigned long long)__hip_atomic_load(abort_word, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0ull,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    drain_stores();
+    __syncthreads();
+    if (threadIdx.x == 0 && seq) __hip_atomic_store(host_out + 10, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
                         unsigned long long* counters, unsigned long long* minbits, hipStream_t s, const uint32_t* abort_word,
-                        unsigned long long* host_out) {
+                        unsigned long long* host_out, unsigned long long seq) {
     // (1024 blocks, one front per thread, measured no faster than 64: more same-address atomics; round 6)
     const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(64, (nf + 255) / 256));
     if (nf <= 0 && host_out == nullptr) return hipSuccess;
-    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, fmin, nf, counters, minbits, abort_word, host_out);
+    hipLaunchKernelGGL(k_count, dim3(blocks), dim3(256), 0, s, fcnt, fstat, fmin, nf, counters, minbits, abort_word, host_out, seq);
     return hipGetLastError();
 }
 

@@ -298,7 +298,8 @@ hipError_t launch_solve_wave(const SolveArgs& A, const int32_t* fronts, int coun
 // counters[0..5] = sums of the per-front pivot records (no same-address atomics inside the factor kernels)
 hipError_t launch_count(const unsigned long long* fcnt, const int32_t* fstat, const double* fmin, int64_t nf,
                         unsigned long long* counters, unsigned long long* minbits, hipStream_t s,
-                        const uint32_t* abort_word = nullptr, unsigned long long* host_out = nullptr);
+                        const uint32_t* abort_word = nullptr, unsigned long long* host_out = nullptr,
+                        unsigned long long seq = 0);  // seq != 0: written to host_out[10] after the rest (host poll)
 // the factorization's device counter block: [0..7] pivot counters, [8] min pivot bits, [9] ||A_pre||_inf bits
 constexpr int kCounterSlots = 11;  // [10]: k_count's block ticket (host_out)
 hipError_t launch_reset_counters(unsigned long long* counters, hipStream_t s);
