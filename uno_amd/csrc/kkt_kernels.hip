@@ -1219,42 +1219,6 @@ __device__ void sym_swap(const S& st, int m, int a, int b, int32_t* lrow, int32_
     }
 }
 
-// sym_swap for one wave on a packed LDS front (m <= 128): every lane computes the two positions it exchanges
-// (none at t == b: A(b, a) stays), all reads before any write (the pairs are disjoint; one wave's LDS accesses
-// are processed in program order), one round trip instead of the four divergent paths' four
-__device__ __forceinline__ void sym_swap_1w(const PackedStore& st, int m, int a, int b, int32_t* lrow, int32_t* lorig) {
-    const int lane = threadIdx.x & 63;
-    int p1[2], p2[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        const int t = lane + 64 * u;
-        int x1 = -1, x2 = -1;
-        if (t < m && t != b) {
-            const int r1 = t <= a ? a : t, c1 = t <= a ? t : a;  // (a, t) | (a, a) | (t, a)
-            const int r2 = t < b ? b : t, c2 = t == a ? b : (t < b ? t : b);  // (b, t) | (b, b) | (t, b)
-            x1 = st.idx(r1, c1);
-            x2 = st.idx(r2, c2);
-        }
-        p1[u] = x1;
-        p2[u] = x2;
-    }
-    double v1[2], v2[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        v1[u] = st.F[p1[u]];
-        v2[u] = st.F[p2[u]];
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-        st.F[p1[u]] = v2[u];
-        st.F[p2[u]] = v1[u];
-    }
-    if (lane == 0) {
-        int32_t y = lrow[a]; lrow[a] = lrow[b]; lrow[b] = y;
-        y = lorig[a]; lorig[a] = lorig[b]; lorig[b] = y;
-    }
-}
-
 // Schur update of the trailing lower triangle after a 1x1 (TWO=false) or 2x2 pivot at k.
 // G x G thread grid, MR row/column blocks per thread, operand columns cached in registers.
 template <int G, int MR, bool TWO, class S>
@@ -1667,16 +1631,14 @@ __device__ void factor_front(const S& st, int m, int p, int32_t* lrow, int32_t* 
         PivotDecision d = sh->dec;
         if (d.kind == PIV_STUCK) { d.kind = PIV_NULL; d.c = k; }
         if (d.c != k) {
-            if constexpr (NT == 64 && !kFullStore<S>) sym_swap_1w(st, m, k, d.c, lrow, lorig);
-            else sym_swap<NT>(st, m, k, d.c, lrow, lorig);
+            sym_swap<NT>(st, m, k, d.c, lrow, lorig);
             __syncthreads();
             fastmask = 0;
         }
         if (d.kind == PIV_2X2_A) {
             int r = d.r == k ? d.c : d.r;
             if (r != k + 1) {
-                if constexpr (NT == 64 && !kFullStore<S>) sym_swap_1w(st, m, k + 1, r, lrow, lorig);
-                else sym_swap<NT>(st, m, k + 1, r, lrow, lorig);
+                sym_swap<NT>(st, m, k + 1, r, lrow, lorig);
                 __syncthreads();
                 fastmask = 0;
             }
