@@ -238,7 +238,11 @@ struct uno_kkt {
     hipEvent_t ev_counters = nullptr;  // after the counters' read-back of the last enqueued factorization
     hipEvent_t ev_wait = nullptr;      // host_wait_stream
     int spin_wait = 1;                 // option "spin_wait": host waits poll (host_wait)
-    int host_flag = 1;                 // option "host_flag": one GPU, the factorization's counters by k_count's flag
+    // option "host_flag" (default 0): one GPU, the host polls k_count's sequence number instead of an event.  Off
+    // by default: the counters and the flag are relaxed system-scope stores ordered only by the storing wave's
+    // vmcnt drain, which does not order their arrival in host memory across fabric paths; a full GPU suite with
+    // it on ended with one failure in the 1465-factorization drop-in trace (unconfirmed: the box was lost)
+    int host_flag = 0;
     unsigned long long count_seq = 0;  // k_count flags issued
     unsigned long long wait_seq = 0;   // the flag the last enqueued factorization writes (0: wait on ev_counters)
     DBuf<unsigned long long> rmaxk;    // front sweeps: n row maxima per sweep (elimination order)
